@@ -1,0 +1,287 @@
+/*
+ * rt2.h — C-ABI of the MI355X-native render path (drop-in for the reference's
+ * GL compute dispatch of RayTracing/Assets/Shaders/compute.glsl).
+ *
+ * Every entry point below replaces one piece of the reference's GPU boundary
+ * (SURVEY.md §8b).  POD layouts are byte-identical to the reference's host
+ * structs so a caller can hand over the very vectors it used to pass to
+ * glBufferData:
+ *
+ *   rt2_triangle  == RTXTriangle      RayTracing/Assets/headers/mesh.h:112-139   (80 B)
+ *   rt2_material  == Material         RayTracing/Assets/headers/mesh.h:26-103    (96 B)
+ *   rt2_node      == Node             RayTracing/Assets/headers/BVH.h:54-65      (48 B)
+ *   rt2_uniforms  == GlobalUniforms   RayTracing/Assets/headers/camera.h:10-36   (192 B, std140)
+ *
+ * Status convention: 0 = ok, < 0 = error; rt2_last_error() returns a
+ * thread-local message.  No C++ exception crosses this ABI.
+ *
+ * Two groups of functions:
+ *   (1) device path  (rt2_scene_*, rt2_render*, rt2_resolve_*) — HIP on gfx950;
+ *   (2) host surface (rt2_sd_*, rt2_camera_*, rt2_write_png) — the reference's
+ *       OBJ/MTL loader, Cornell-box builders, BVH build, camera and PNG writer,
+ *       restated in C++ behind the same ABI.
+ */
+#ifndef RT2_H
+#define RT2_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT2_ABI_VERSION 1
+
+/* Material types: mesh.h:16-22 == compute.glsl:7-13 */
+enum {
+    RT2_DIFFUSE = 0,
+    RT2_SPECULAR = 1,
+    RT2_LIGHT = 2,
+    RT2_CHECKER = 3,
+    RT2_GLASS = 4,
+    RT2_TEXTURE = 5,
+    RT2_GLASS_HIGHLIGHT = 6
+};
+
+typedef struct rt2_vec4 { float x, y, z, w; } rt2_vec4;
+typedef struct rt2_vec2 { float x, y; } rt2_vec2;
+
+/* RTXTriangle, mesh.h:112-139.  GLSL std430 `Triangle` (compute.glsl:46-56)
+ * reads a/b/c at byte 0/16/32, the UVs at 48/56/64 and mtlIndex at 72. */
+typedef struct rt2_triangle {
+    rt2_vec4 a, b, c;
+    rt2_vec2 aTex, bTex, cTex;
+    int32_t materialIndex;
+    float pad;
+} rt2_triangle;
+
+/* Material, mesh.h:26-103 == compute.glsl:17-37 */
+typedef struct rt2_material {
+    rt2_vec4 color;
+    rt2_vec4 specularColor;
+    rt2_vec4 emissionColor;
+    int32_t textureIndex;
+    float emissionStrength;
+    float smoothness;
+    float specularProbability;
+    float checkerScale;
+    float refractiveIndex;
+    int32_t materialType;
+    int32_t index;
+    int32_t isEdgeHighlight;
+    int32_t pad1, pad2, pad3;
+} rt2_material;
+
+/* Node + BoundingBox, BVH.h:11-65 == compute.glsl:58-73 */
+typedef struct rt2_node {
+    float bmin[3];
+    float pad0;
+    float bmax[3];
+    float pad1;
+    int32_t triangleIndex;
+    int32_t triangleCount;
+    int32_t childIndex;
+    int32_t pad;
+} rt2_node;
+
+/* GlobalUniforms, camera.h:10-36 == compute.glsl:119-146 (std140) */
+typedef struct rt2_uniforms {
+    int32_t pad;
+    int32_t numTextures;
+    uint32_t width;
+    uint32_t height;
+    int32_t numSpheres;
+    int32_t numTriangles;
+    int32_t basicShading;
+    int32_t basicShadingShadow;
+    rt2_vec4 basicShadingLightPosition;
+    int32_t environmentalLight;
+    int32_t maxBounceCount;
+    int32_t numRaysPerPixel;
+    uint32_t frameIndex;
+    rt2_vec4 cameraPos;
+    rt2_vec4 viewportRight;
+    rt2_vec4 viewportUp;
+    rt2_vec4 viewportFront;
+    rt2_vec4 pixelRight;
+    rt2_vec4 pixelUp;
+    rt2_vec4 defocusDiskRight;
+    rt2_vec4 defocusDiskUp;
+} rt2_uniforms;
+
+/* Image-row shard: the rows y in [0, height) with
+ *   (y / tile_rows) % nranks == rank
+ * in increasing order form this rank's slab (SURVEY.md §8e, row-tile
+ * interleave).  {1, 0, 1} is the whole image. */
+typedef struct rt2_shard {
+    int32_t tile_rows;
+    int32_t rank;
+    int32_t nranks;
+} rt2_shard;
+
+/* Work counters of the last render on a scene (SURVEY.md §8d units). */
+typedef struct rt2_stats {
+    uint64_t samples;   /* pixel-rays traced = pixels * R * F              */
+    uint64_t segments;  /* closest-hit queries (bounces actually traced)     */
+    uint64_t tests;     /* ray-triangle tests = segments * N (brute force)   */
+} rt2_stats;
+
+const char* rt2_last_error(void);
+int rt2_abi_version(void);
+
+/* ------------------------------------------------------------------------
+ * (1) Device path
+ * ---------------------------------------------------------------------- */
+
+typedef struct rt2_scene rt2_scene;
+
+/* Replaces the three SSBO uploads (rayTracing.cpp:1323-1325, SSBO.cpp:3-10,
+ * glBufferData GL_STATIC_DRAW: the arrays are copied, the caller keeps
+ * ownership).  `nodes` may be NULL (brute-force traversal does not need it).
+ * Materials with materialType TEXTURE sample nothing yet (numTextures = 0
+ * semantics of compute.glsl:349-350: black attenuation). */
+int rt2_scene_create(const rt2_triangle* tris, int32_t n_tris,
+                     const rt2_material* mats, int32_t n_mats,
+                     const rt2_node* nodes, int32_t n_nodes,
+                     int32_t device, rt2_scene** out);
+void rt2_scene_destroy(rt2_scene* scene);
+
+/* Number of slab rows a shard owns for an image of `height` rows. */
+int32_t rt2_shard_rows(int32_t height, rt2_shard shard);
+/* Image row y of slab row `local_row` (inverse of the interleave). */
+int32_t rt2_shard_row(int32_t local_row, rt2_shard shard);
+
+/* Replaces `frame_count` consecutive glDispatchCompute calls of compute.glsl
+ * (rayTracing.cpp:184-191, uniforms->frameIndex = frame_begin + i), restricted
+ * to the shard's rows, with the per-frame rgba32f imageStore (compute.glsl:700)
+ * folded into an accumulator instead of a texture:
+ *
+ *   d_accum[4*(slab_row*W + x) + c] += color_f[c]   for f = frame_begin ...
+ *
+ * in increasing frame order (so splitting the frames over several calls gives
+ * bit-identical sums).  d_accum is DEVICE memory of rows*W*4 floats.
+ * d_accum8 (nullable, device, rows*W*4 uint32) accumulates the per-frame GL
+ * unorm8 quantisation of the same colours — the reference screenshot path
+ * (rayTracing.cpp:217-238).  `stream` is a hipStream_t (NULL = default);
+ * the call is asynchronous like glDispatchCompute.  uniforms->basicShading
+ * must be 0 (the one-ray preview traceBasic is not on this path). */
+int rt2_render(rt2_scene* scene, const rt2_uniforms* uniforms,
+               uint32_t frame_begin, uint32_t frame_count, rt2_shard shard,
+               float* d_accum, uint32_t* d_accum8, void* stream);
+
+/* Blocking convenience wrapper: renders into internal device buffers and
+ * copies the resolved mean image back to host memory.  out_rgba (nullable):
+ * rows*W*4 floats, mean over the frames (alpha = 1), slab-row order, slab row
+ * 0 = lowest image row (GL convention, row 0 = bottom).  out_rgb8 (nullable):
+ * rows*W*3 bytes, the reference's 8-bit screenshot average
+ * (rayTracing.cpp:248-250), NOT flipped. */
+int rt2_render_host(rt2_scene* scene, const rt2_uniforms* uniforms,
+                    uint32_t frame_begin, uint32_t frame_count, rt2_shard shard,
+                    float* out_rgba, uint8_t* out_rgb8);
+
+/* Device resolve: out[i] = accum[i] / frames (rgb), alpha = 1.  Async. */
+int rt2_resolve_rgba32f(const float* d_accum, int64_t n_pixels, uint32_t frames,
+                        float* d_out, void* stream);
+/* Host resolve of the 8-bit reference path (rayTracing.cpp:248-250):
+ * u8(min(255, float(sum)/frames)) per channel, rgba sums -> rgb bytes. */
+int rt2_resolve_rgb8_reference(const uint32_t* accum8, int64_t n_pixels, uint32_t frames,
+                               uint8_t* out_rgb);
+
+/* Counters of the renders issued on this scene since the last reset
+ * (synchronises the scene's device). */
+int rt2_scene_stats(rt2_scene* scene, rt2_stats* out, int reset);
+
+/* Kernel-variant control for experiments: 0 = auto.  Returns the variant the
+ * next render will use for this scene. */
+int rt2_scene_set_variant(rt2_scene* scene, int variant);
+
+/* ------------------------------------------------------------------------
+ * (2) Host surface
+ * ---------------------------------------------------------------------- */
+
+/* Scene data under construction: the reference's rtxTriangles, bvhTriangles,
+ * materials, texture list and BVH nodes (rayTracing.cpp:1256-1293). */
+typedef struct rt2_scene_data rt2_scene_data;
+
+rt2_scene_data* rt2_sd_create(void);
+void rt2_sd_destroy(rt2_scene_data* sd);
+
+/* getTrianglesData_ (mesh.h:279-613): first *.obj of the folder, every *.mtl
+ * of the folder, texture names from <folder>/textures. Appends. */
+int rt2_sd_load_obj_folder(rt2_scene_data* sd, const char* folder);
+/* Appends one material; returns its index or < 0. */
+int32_t rt2_sd_add_material(rt2_scene_data* sd, const rt2_material* m);
+/* Appends one triangle (and its BVH triangle) as a builder would. */
+int rt2_sd_add_triangle(rt2_scene_data* sd, const float a[3], const float b[3], const float c[3],
+                        int32_t material_index);
+
+/* Appends n complete triangle records (rtxTriangles.push_back). */
+int rt2_sd_add_triangles(rt2_scene_data* sd, const rt2_triangle* tris, int32_t n);
+
+/* Scene builders of rayTracing.cpp. */
+int rt2_sd_add_cornell_box(rt2_scene_data* sd, float light_size, float pad, int32_t light_mtl,
+                           int32_t light_enabled);                           /* :453-547 */
+int rt2_sd_add_mirror_cornell_box(rt2_scene_data* sd, float light_size, float pad,
+                                  int32_t light_mtl, int32_t mirror_mtl);    /* :569-664 */
+int rt2_sd_add_side_lit_cornell_box(rt2_scene_data* sd, float light_size, float pad,
+                                    int32_t light_mtl, int32_t wall_mtl, int32_t rotate); /* :690-847 */
+int rt2_sd_add_sky_light_plane(rt2_scene_data* sd, int32_t light_mtl);       /* :388-432 */
+int rt2_sd_add_cube(rt2_scene_data* sd, const float center[3], const float size[3],
+                    const float rotation[3], int32_t mtl);                   /* :867-923 */
+int rt2_sd_create_classic_cornell_box(rt2_scene_data* sd, float room, int32_t red, int32_t green,
+                                      int32_t white, int32_t light);         /* :949-1041 */
+int rt2_sd_create_diverse_cornell_box(rt2_scene_data* sd, float room, int32_t red, int32_t green,
+                                      int32_t white, int32_t light, int32_t glass, int32_t mirror,
+                                      int32_t checker, int32_t metal);       /* :1071-1118 */
+
+/* BVH(bvhTriangles, rtxTriangles) (BVH.h:145-221): builds the node array and
+ * reorders the triangles in place, exactly as the reference does. */
+int rt2_sd_build_bvh(rt2_scene_data* sd);
+
+int32_t rt2_sd_num_triangles(const rt2_scene_data* sd);
+int32_t rt2_sd_num_materials(const rt2_scene_data* sd);
+int32_t rt2_sd_num_nodes(const rt2_scene_data* sd);
+int32_t rt2_sd_num_textures(const rt2_scene_data* sd);
+const rt2_triangle* rt2_sd_triangles(const rt2_scene_data* sd);
+const rt2_material* rt2_sd_materials(const rt2_scene_data* sd);
+const rt2_node* rt2_sd_nodes(const rt2_scene_data* sd);
+/* BVHTriangle min/max/center (mesh.h:141-154), 9 floats per triangle. */
+int rt2_sd_bvh_triangles(const rt2_scene_data* sd, float* out9);
+/* Texture file name i (directory order, mesh.h:305-318) or NULL. */
+const char* rt2_sd_texture_name(const rt2_scene_data* sd, int32_t i);
+
+/* Material helpers of mesh.h:47-102 (fields the reference leaves
+ * uninitialised are zero here). */
+void rt2_material_default(rt2_material* m);
+void rt2_material_make_diffuse(rt2_material* m, float r, float g, float b);
+void rt2_material_make_light(rt2_material* m, float r, float g, float b, float strength);
+void rt2_material_make_specular(rt2_material* m, float r, float g, float b,
+                                float sr, float sg, float sb, float smooth, float prob);
+void rt2_material_make_checker(rt2_material* m, float scale);
+void rt2_material_make_glass(rt2_material* m, float r, float g, float b, float ior);
+
+/* Camera(...) + updateUniforms (camera.h:99-192): fills the eight camera
+ * vec4s of `u` (other fields untouched). */
+typedef struct rt2_camera {
+    int32_t width, height;
+    float position[3];
+    float hfov, pitch, yaw;
+    float focus_distance, defocus_angle, zoom;
+} rt2_camera;
+/* Reference defaults (rayTracing.cpp:82-89) for a width x height screen. */
+void rt2_camera_default(rt2_camera* cam, int32_t width, int32_t height);
+int rt2_camera_uniforms(const rt2_camera* cam, rt2_uniforms* u);
+/* Offline-render uniforms (rayTracing.cpp:146-153 + :1386-1400). */
+void rt2_uniforms_offline(rt2_uniforms* u, int32_t width, int32_t height, int32_t max_bounce,
+                          int32_t rays_per_pixel, int32_t num_triangles, int32_t num_textures);
+
+/* stbi_write_png surface (rayTracing.cpp:264): 8-bit, comps 1..4. */
+int rt2_write_png(const char* path, int32_t w, int32_t h, int32_t comps, const uint8_t* data,
+                  int32_t stride_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT2_H */

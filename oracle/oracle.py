@@ -1,0 +1,86 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes wrapper of oracle/liboracle.so, the CPU
+restatement of compute.glsl (rt_oracle.c).  Imported by tests/, by
+__graft_entry__.smoke() and by bench.py's cpu_baseline leg; never by the
+product package.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+REF_DUMP = os.path.join(HERE, "_ref", "ref_dump")
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-C", HERE, "liboracle.so"], check=True, stdout=subprocess.DEVNULL)
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = C.CDLL(LIB)
+        P = C.c_void_p
+        L.oracle_render.restype = C.c_int
+        L.oracle_render.argtypes = [P, C.c_int32, P, C.c_int32, P, C.c_int32, P, C.c_uint32, C.c_uint32, P,
+                                    C.c_int32, C.c_int32, C.c_int32, P, P, P, P]
+        L.oracle_pcg_next.restype = C.c_uint32
+        L.oracle_pcg_next.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_float)]
+        L.oracle_ray_triangle.restype = C.c_int
+        L.oracle_ray_triangle.argtypes = [P, P, P, P]
+        L.oracle_sky.restype = None
+        L.oracle_sky.argtypes = [P, P]
+        L.oracle_tonemap_srgb.restype = C.c_float
+        L.oracle_tonemap_srgb.argtypes = [C.c_float]
+        L.oracle_pinned.restype = C.c_float
+        L.oracle_pinned.argtypes = [C.c_int, C.c_float]
+        _lib = L
+    return _lib
+
+
+def render(triangles: np.ndarray, materials: np.ndarray, uniforms, rows, frame_begin: int = 0,
+           frame_count: int = 1, mode: str = "brute", nodes: np.ndarray | None = None, threads: int | None = None,
+           with_acc8: bool = False):
+    """Renders the listed image rows.  Returns (accum[nrows, W, 4] = per-pixel SUM over
+    frames, acc8 or None, segments, tests)."""
+    tri = np.ascontiguousarray(triangles)
+    mat = np.ascontiguousarray(materials)
+    assert tri.dtype.itemsize == 80 and mat.dtype.itemsize == 96
+    rows = np.ascontiguousarray(rows, dtype=np.int32)
+    W = int(uniforms.width)
+    acc = np.zeros((len(rows), W, 4), dtype=np.float32)
+    acc8 = np.zeros((len(rows), W, 4), dtype=np.uint32) if with_acc8 else None
+    segs = C.c_uint64(0)
+    tests = C.c_uint64(0)
+    nd = None if nodes is None else np.ascontiguousarray(nodes)
+    m = {"brute": 0, "bvh": 1}[mode]
+    rc = lib().oracle_render(tri.ctypes.data, len(tri), mat.ctypes.data, len(mat),
+                             None if nd is None else nd.ctypes.data, 0 if nd is None else len(nd),
+                             C.addressof(uniforms), frame_begin, frame_count, rows.ctypes.data, len(rows), m,
+                             threads or os.cpu_count() or 1, acc.ctypes.data,
+                             None if acc8 is None else acc8.ctypes.data, C.byref(segs), C.byref(tests))
+    if rc != 0:
+        raise RuntimeError(f"oracle_render failed: {rc}")
+    return acc, acc8, segs.value, tests.value
+
+
+def pcg_sequence(seed: int, n: int):
+    s = C.c_uint32(seed)
+    f = C.c_float()
+    out = []
+    for _ in range(n):
+        r = lib().oracle_pcg_next(C.byref(s), C.byref(f))
+        out.append((r, f.value))
+    return out
+
+
+def pinned(which: int, x: float) -> float:
+    return lib().oracle_pinned(which, x)

@@ -1,0 +1,733 @@
+// MI355X (gfx950) render path: the per-pixel Monte-Carlo loop of
+// RayTracing/Assets/Shaders/compute.glsl:472-701 as a persistent HIP kernel.
+//
+// Unit of work ("item") = one pixel of the shard; an item runs frames
+// frame_begin.. in order, each frame numRaysPerPixel rays in order, exactly
+// like one compute.glsl invocation per frame (the rays of a pixel-frame share
+// one sequential RNG stream, compute.glsl:668/683, so they cannot be split).
+//
+// Execution model:
+//   - one lane = one item at a time; every loop iteration each lane traces ONE
+//     segment (closest-hit query + scatter) of its current ray;
+//   - a lane whose path ends starts the next ray / frame of its item itself;
+//     a lane whose item ends is refilled from a global item counter with one
+//     wave-level __ballot + popcount + mbcnt prefix sum + one atomicAdd per
+//     wave (ray regeneration: lanes never idle while items remain);
+//   - closest hit = brute force over all triangles in array order (strict <,
+//     so the lowest index wins a tie).  Triangles are pre-transformed on the
+//     device to {a, e0 = b-a, e1 = c-a, n = cross(e0,e1)} (48 B, bit-identical
+//     to computing them per test) and staged in LDS:
+//       RESIDENT: the whole array fits in LDS, loaded once per workgroup, and
+//                 waves then run independently (no barriers);
+//       TILED:    the array is streamed through LDS in tiles; the workgroup
+//                 sweeps every tile in lockstep once per segment.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../../include/rt2.h"
+#include "rt2_math.h"
+
+using namespace rt2d;
+
+namespace {
+
+constexpr int kWave = 64;
+
+struct RenderParams {
+    const float4* tri;  // 3 float4 per triangle: {ax ay az e0x} {e0y e0z e1x e1y} {e1z nx ny nz}
+    const int* tri_mtl;
+    const rt2_material* mats;
+    int n_tris;
+    int n_mats;
+    int W, H;
+    int maxBounce, R, envLight;
+    float cam[3], vpRight[3], vpUp[3], vpFront[3], pixR[3], pixU[3], defR[3], defU[3];
+    uint32_t frame_begin, frame_count;
+    int tile_rows, rank, nranks;
+    unsigned long long n_items;
+    float4* accum;
+    uint4* accum8;
+    unsigned long long* item_counter;
+    unsigned long long* seg_counter;
+    int tile_tris;  // TILED: triangles per LDS tile
+};
+
+enum : int { ST_NEED_ITEM = 0, ST_NEW_FRAME = 1, ST_NEW_RAY = 2, ST_TRACE = 3, ST_DONE = 4 };
+
+__device__ __forceinline__ f3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
+__device__ __forceinline__ f3 xyz4(const rt2_vec4& v) { return mk(v.x, v.y, v.z); }
+
+__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+__device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ int shard_row(int local_row, int tile_rows, int rank, int nranks) {
+    int t = local_row / tile_rows;
+    return (t * nranks + rank) * tile_rows + local_row % tile_rows;
+}
+
+// One Möller–Trumbore test (compute.glsl:302-340) against a pre-transformed
+// triangle; updates the running closest hit (compute.glsl:432-434).
+__device__ __forceinline__ void mt_test(const f3& o, const f3& d, float4 t0, float4 t1, float4 t2, int idx,
+                                        float& best, int& best_i) {
+    const f3 a = mk(t0.x, t0.y, t0.z);
+    const f3 e0 = mk(t0.w, t1.x, t1.y);
+    const f3 e1 = mk(t1.z, t1.w, t2.x);
+    const f3 n = mk(t2.y, t2.z, t2.w);
+    float det = -dot(d, n);
+    bool ok = !((det < 1e-10f && det > -1e-10f) || det < 0.0f);
+    float inv = 1.0f / det;
+    f3 ao = sub(o, a);
+    float dst = dot(ao, n) * inv;
+    ok = ok && !(dst <= 1e-6f);
+    f3 q = cross(d, ao);
+    float u = -dot(e1, q) * inv;
+    float v = dot(e0, q) * inv;
+    ok = ok && !(u < 0.0f || v < 0.0f || 1.0f - u - v < 0.0f);
+    if (ok && dst < best) {
+        best = dst;
+        best_i = idx;
+    }
+}
+
+struct Lane {
+    int st;
+    unsigned long long item;
+    int x, y;
+    uint32_t frame;  // frames done for this item
+    uint32_t seed;
+    int ray;
+    int bounce;
+    bool inside;
+    f3 o, d, rayColor, incoming, colorCum, endPoint;
+    f3 acc;
+    uint32_t a8x, a8y, a8z;
+    uint32_t segs;
+};
+
+__device__ __forceinline__ void end_path(Lane& L, const RenderParams& p);
+
+// Phase A: bring every lane to ST_TRACE or ST_DONE (wave-collective).
+__device__ __forceinline__ void advance(Lane& L, const RenderParams& p) {
+    for (;;) {
+        const bool need = L.st == ST_NEED_ITEM;
+        const unsigned long long m = __ballot(need);
+        if (m) {
+            unsigned long long base = 0;
+            if (lane_id() == 0) base = atomicAdd(p.item_counter, (unsigned long long)__popcll(m));
+            base = __shfl(base, 0);
+            if (need) {
+                unsigned long long it = base + lanes_below(m);
+                if (it < p.n_items) {
+                    L.item = it;
+                    int lr = (int)(it / (unsigned long long)p.W);
+                    L.x = (int)(it - (unsigned long long)lr * (unsigned long long)p.W);
+                    L.y = shard_row(lr, p.tile_rows, p.rank, p.nranks);
+                    L.frame = 0;
+                    float4 a = p.accum[it];
+                    L.acc = mk(a.x, a.y, a.z);
+                    if (p.accum8) {
+                        uint4 q = p.accum8[it];
+                        L.a8x = q.x;
+                        L.a8y = q.y;
+                        L.a8z = q.z;
+                    }
+                    L.st = ST_NEW_FRAME;
+                } else {
+                    L.st = ST_DONE;
+                }
+            }
+        }
+        if (L.st == ST_NEW_FRAME) {
+            // compute.glsl:662-670
+            const uint32_t f = p.frame_begin + L.frame;
+            float px = (float)(L.x * 2 - p.W) / (float)p.W;
+            float py = (float)(L.y * 2 - p.H) / (float)p.H;
+            L.seed = (uint32_t)L.x + (uint32_t)L.y * (uint32_t)p.W + f * 968824447u;
+            L.endPoint = add(add(add(ld3(p.cam), ld3(p.vpFront)), muls(ld3(p.vpRight), px)), muls(ld3(p.vpUp), py));
+            L.colorCum = mk(0.0f, 0.0f, 0.0f);
+            L.ray = 0;
+            L.st = ST_NEW_RAY;
+        }
+        if (L.st == ST_NEW_RAY) {
+            // compute.glsl:685-690
+            float ang = rnd(L.seed);
+            float cs = rt2pm_cosf(ang), sn = rt2pm_sinf(ang);
+            L.o = add(add(ld3(p.cam), muls(ld3(p.defR), cs)), muls(ld3(p.defU), sn));
+            float jr = -0.5f + (0.5f - -0.5f) * rnd(L.seed);
+            float ju = -0.5f + (0.5f - -0.5f) * rnd(L.seed);
+            f3 endJ = add(add(L.endPoint, muls(ld3(p.pixR), jr)), muls(ld3(p.pixU), ju));
+            L.d = normalize(sub(endJ, L.o));
+            L.inside = false;
+            L.rayColor = mk(1.0f, 1.0f, 1.0f);
+            L.incoming = mk(0.0f, 0.0f, 0.0f);
+            L.bounce = 0;
+            L.st = ST_TRACE;
+            if (p.maxBounce <= 0) end_path(L, p);  // trace() returns 0 without tracing
+        }
+        if (!__any(L.st != ST_TRACE && L.st != ST_DONE)) break;
+    }
+}
+
+// End of a path: colorCumulative += trace(...) (compute.glsl:692); next ray,
+// or end of the frame (compute.glsl:696-700 + the screenshot accumulation).
+__device__ __forceinline__ void end_path(Lane& L, const RenderParams& p) {
+    L.colorCum = add(L.colorCum, L.incoming);
+    L.ray += 1;
+    if (L.ray < p.R) {
+        L.st = ST_NEW_RAY;
+        return;
+    }
+    f3 c = divs(L.colorCum, (float)p.R);
+    c = mk(srgb1(aces1(c.x)), srgb1(aces1(c.y)), srgb1(aces1(c.z)));
+    L.acc = add(L.acc, c);
+    // GL float -> unorm8, round to nearest (GL 4.3 §2.3.5.2)
+    L.a8x += (uint32_t)(clampf(c.x, 0.0f, 1.0f) * 255.0f + 0.5f);
+    L.a8y += (uint32_t)(clampf(c.y, 0.0f, 1.0f) * 255.0f + 0.5f);
+    L.a8z += (uint32_t)(clampf(c.z, 0.0f, 1.0f) * 255.0f + 0.5f);
+    L.frame += 1;
+    if (L.frame < p.frame_count) {
+        L.st = ST_NEW_FRAME;
+        return;
+    }
+    p.accum[L.item] = make_float4(L.acc.x, L.acc.y, L.acc.z, 0.0f);
+    if (p.accum8) p.accum8[L.item] = make_uint4(L.a8x, L.a8y, L.a8z, 0u);
+    L.st = ST_NEED_ITEM;
+}
+
+// Phase C: scatter at the closest hit (compute.glsl:485-559).
+__device__ __forceinline__ void shade(Lane& L, const RenderParams& p, float best, int bi) {
+    if (bi >= 0) {
+        const float4 t2 = p.tri[3 * bi + 2];
+        const f3 normal = normalize(mk(t2.y, t2.z, t2.w));  // normalize(cross01), compute.glsl:331
+        const f3 hitPoint = add(L.o, muls(L.d, best));      // compute.glsl:330
+        const rt2_material m = p.mats[p.tri_mtl[bi]];
+        if (m.materialType != RT2_GLASS)
+            L.o = sub(hitPoint, muls(muls(L.d, best), -1e-3f));
+        else
+            L.o = add(hitPoint, muls(muls(L.d, best), -1e-3f));
+        f3 atten = mk(0.0f, 0.0f, 0.0f);
+        const f3 prevDir = L.d;
+        switch (m.materialType) {
+        case RT2_DIFFUSE:
+        case RT2_TEXTURE:
+            L.d = normalize(add(normal, rnd_dir(L.seed)));
+            atten = m.materialType == RT2_DIFFUSE ? xyz4(m.color) : mk(0.0f, 0.0f, 0.0f);
+            break;
+        case RT2_SPECULAR: {
+            f3 diffuseDir = normalize(add(normal, rnd_dir(L.seed)));
+            f3 specDir = reflect(L.d, normal);
+            bool isSpec = m.specularProbability > rnd(L.seed);
+            L.d = mixs(diffuseDir, specDir, isSpec ? m.smoothness : 0.0f);
+            atten = isSpec ? mk(1.0f, 1.0f, 1.0f) : xyz4(m.color);
+            break;
+        }
+        case RT2_LIGHT: {
+            f3 emitted = muls(xyz4(m.emissionColor), m.emissionStrength);
+            L.incoming = add(L.incoming, mul(emitted, L.rayColor));
+            end_path(L, p);
+            return;
+        }
+        case RT2_CHECKER: {
+            L.d = normalize(add(normal, rnd_dir(L.seed)));
+            float s = m.checkerScale;
+            bool black = false;
+            if (s > 0.0f) {
+                float sum = floorf(L.o.x * s) + floorf(L.o.y * s) + floorf(L.o.z * s);
+                float md = sum - 2.0f * floorf(sum / 2.0f);
+                black = md == 0.0f;
+            }
+            atten = black ? mk(0.0f, 0.0f, 0.0f) : mk(1.0f, 1.0f, 1.0f);
+            break;
+        }
+        case RT2_GLASS: {
+            float eta = L.inside ? m.refractiveIndex : 1.0f / m.refractiveIndex;
+            bool refr;
+            L.d = refract_(L.d, normal, eta, refr);
+            L.inside = refr != L.inside;
+            atten = xyz4(m.color);
+            break;
+        }
+        default:  // GLASS_HIGHLIGHT and unknown types: trace() returns magenta
+            L.incoming = mk(1.0f, 0.0f, 1.0f);
+            end_path(L, p);
+            return;
+        }
+        if (m.isEdgeHighlight && L.bounce > 1)
+            L.d = prevDir;
+        else
+            L.rayColor = mul(L.rayColor, atten);
+        float pr = fmaxf(L.rayColor.x, fmaxf(L.rayColor.y, L.rayColor.z));
+        if (rnd(L.seed) > pr) {
+            end_path(L, p);
+            return;
+        }
+        L.rayColor = muls(L.rayColor, 1.0f / pr);
+        if (L.bounce >= p.maxBounce) end_path(L, p);
+    } else {
+        if (p.envLight) L.incoming = add(L.incoming, mul(sky(L.d), L.rayColor));
+        end_path(L, p);
+    }
+}
+
+__device__ __forceinline__ void lane_init(Lane& L) {
+    L.st = ST_NEED_ITEM;
+    L.item = 0;
+    L.x = L.y = 0;
+    L.frame = 0;
+    L.seed = 0;
+    L.ray = 0;
+    L.bounce = 0;
+    L.inside = false;
+    L.o = L.d = L.rayColor = L.incoming = L.colorCum = L.endPoint = L.acc = mk(0.0f, 0.0f, 0.0f);
+    L.a8x = L.a8y = L.a8z = 0;
+    L.segs = 0;
+}
+
+__device__ __forceinline__ void flush_counters(const Lane& L, const RenderParams& p) {
+    unsigned long long s = L.segs;
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    if (lane_id() == 0) atomicAdd(p.seg_counter, s);
+}
+
+// RESIDENT: all triangles in LDS, waves independent after the initial load.
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void render_resident(RenderParams p) {
+    extern __shared__ float4 lds[];
+    const int n4 = 3 * p.n_tris;
+    for (int i = threadIdx.x; i < n4; i += BLOCK) lds[i] = p.tri[i];
+    __syncthreads();
+
+    Lane L;
+    lane_init(L);
+    for (;;) {
+        advance(L, p);
+        if (!__any(L.st == ST_TRACE)) break;
+        if (L.st == ST_TRACE) {
+            L.bounce += 1;
+            L.segs += 1;
+            float best = 1e38f;
+            int bi = -1;
+            const f3 o = L.o, d = L.d;
+#pragma unroll 4
+            for (int i = 0; i < p.n_tris; i++) {
+                mt_test(o, d, lds[3 * i], lds[3 * i + 1], lds[3 * i + 2], i, best, bi);
+            }
+            shade(L, p, best, bi);
+        }
+    }
+    flush_counters(L, p);
+}
+
+// TILED: triangles streamed through LDS; the workgroup sweeps in lockstep.
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void render_tiled(RenderParams p) {
+    extern __shared__ float4 lds[];
+    __shared__ int block_any;
+    Lane L;
+    lane_init(L);
+    const int T = p.tile_tris;
+    for (;;) {
+        advance(L, p);
+        if (threadIdx.x == 0) block_any = 0;
+        __syncthreads();
+        if (L.st == ST_TRACE) block_any = 1;
+        __syncthreads();
+        if (!block_any) break;
+        const bool tracing = L.st == ST_TRACE;
+        float best = 1e38f;
+        int bi = -1;
+        const f3 o = L.o, d = L.d;
+        for (int base = 0; base < p.n_tris; base += T) {
+            const int cnt = min(T, p.n_tris - base);
+            __syncthreads();
+            for (int i = threadIdx.x; i < 3 * cnt; i += BLOCK) lds[i] = p.tri[3 * base + i];
+            __syncthreads();
+            if (tracing) {
+#pragma unroll 4
+                for (int i = 0; i < cnt; i++) mt_test(o, d, lds[3 * i], lds[3 * i + 1], lds[3 * i + 2], base + i, best, bi);
+            }
+        }
+        if (tracing) {
+            L.bounce += 1;
+            L.segs += 1;
+            shade(L, p, best, bi);
+        }
+    }
+    flush_counters(L, p);
+}
+
+// Pre-transform: RTXTriangle (80 B) -> {a, e0, e1, n} (48 B) + material index.
+__global__ void prep_triangles(const rt2_triangle* tris, int n, float4* out, int* mtl) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const rt2_triangle t = tris[i];
+    const f3 a = xyz4(t.a), b = xyz4(t.b), c = xyz4(t.c);
+    const f3 e0 = sub(b, a), e1 = sub(c, a);
+    const f3 nn = cross(e0, e1);
+    out[3 * i + 0] = make_float4(a.x, a.y, a.z, e0.x);
+    out[3 * i + 1] = make_float4(e0.y, e0.z, e1.x, e1.y);
+    out[3 * i + 2] = make_float4(e1.z, nn.x, nn.y, nn.z);
+    mtl[i] = t.materialIndex;
+}
+
+__global__ void resolve_kernel(const float4* acc, long long n, float inv_frames_dummy, float frames, float4* out) {
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    (void)inv_frames_dummy;
+    float4 a = acc[i];
+    out[i] = make_float4(a.x / frames, a.y / frames, a.z / frames, 1.0f);
+}
+
+// Numerics self-test: the IEEE primitives and pinned functions the path uses,
+// evaluated on the device for comparison with the host (tests/test_gpu_numerics.py).
+__global__ void selftest_kernel(const float* in, int n, float* out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float x = in[i];
+    float y = in[(i * 7 + 3) % n];
+    out[10 * i + 0] = x / y;
+    out[10 * i + 1] = __builtin_sqrtf(fabsf(x));
+    out[10 * i + 2] = __builtin_fmaf(x, y, x);
+    out[10 * i + 3] = rt2pm_expf(x);
+    out[10 * i + 4] = rt2pm_logf(fabsf(x));
+    out[10 * i + 5] = rt2pm_acosf(fmaxf(-1.0f, fminf(1.0f, y)));
+    out[10 * i + 6] = rt2pm_cosf(x);
+    out[10 * i + 7] = rt2pm_sinf(x);
+    out[10 * i + 8] = rt2pm_powf(fabsf(y), 1.0f / 2.2f);
+    out[10 * i + 9] = 1.0f / x;
+}
+
+}  // namespace
+
+/* =========================================================================
+ * C-ABI, device half
+ * ======================================================================= */
+namespace rt2h {
+void set_error(const std::string& msg);
+}
+
+#define HIPCHECK(expr)                                                                         \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess) {                                                                \
+            rt2h::set_error(std::string(#expr) + ": " + hipGetErrorString(e_));                \
+            return -1;                                                                         \
+        }                                                                                      \
+    } while (0)
+
+struct rt2_scene {
+    int device = 0;
+    int n_tris = 0, n_mats = 0, n_nodes = 0;
+    rt2_triangle* d_raw = nullptr;
+    float4* d_tri = nullptr;
+    int* d_mtl = nullptr;
+    rt2_material* d_mats = nullptr;
+    rt2_node* d_nodes = nullptr;
+    unsigned long long* d_counters = nullptr;  // [0] item counter, [1] segments
+    unsigned long long samples = 0, tests_per_seg = 0;
+    int variant = 0;
+    int num_cus = 256;
+    size_t max_lds = 65536;
+};
+
+extern "C" int rt2_scene_create(const rt2_triangle* tris, int32_t n_tris, const rt2_material* mats, int32_t n_mats,
+                                const rt2_node* nodes, int32_t n_nodes, int32_t device, rt2_scene** out) {
+    if (!out || n_tris < 0 || n_mats < 1 || !mats || (n_tris > 0 && !tris)) {
+        rt2h::set_error("rt2_scene_create: bad argument");
+        return -1;
+    }
+    for (int i = 0; i < n_tris; i++) {
+        if (tris[i].materialIndex < 0 || tris[i].materialIndex >= n_mats) {
+            rt2h::set_error("rt2_scene_create: triangle " + std::to_string(i) + " has material index " +
+                            std::to_string(tris[i].materialIndex) + " outside [0, " + std::to_string(n_mats) + ")");
+            return -1;
+        }
+    }
+    int ndev = 0;
+    HIPCHECK(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) {
+        rt2h::set_error("rt2_scene_create: no HIP device " + std::to_string(device));
+        return -1;
+    }
+    HIPCHECK(hipSetDevice(device));
+    rt2_scene* s = new rt2_scene();
+    s->device = device;
+    s->n_tris = n_tris;
+    s->n_mats = n_mats;
+    s->n_nodes = nodes ? n_nodes : 0;
+    hipDeviceProp_t prop;
+    HIPCHECK(hipGetDeviceProperties(&prop, device));
+    s->num_cus = prop.multiProcessorCount;
+    s->max_lds = prop.maxSharedMemoryPerMultiProcessor ? prop.maxSharedMemoryPerMultiProcessor : 65536;
+    const size_t nt = (size_t)std::max(n_tris, 1);
+    HIPCHECK(hipMalloc(&s->d_raw, nt * sizeof(rt2_triangle)));
+    HIPCHECK(hipMalloc(&s->d_tri, nt * 3 * sizeof(float4)));
+    HIPCHECK(hipMalloc(&s->d_mtl, nt * sizeof(int)));
+    HIPCHECK(hipMalloc(&s->d_mats, (size_t)n_mats * sizeof(rt2_material)));
+    HIPCHECK(hipMalloc(&s->d_counters, 4 * sizeof(unsigned long long)));
+    HIPCHECK(hipMemset(s->d_counters, 0, 4 * sizeof(unsigned long long)));
+    if (n_tris > 0) HIPCHECK(hipMemcpy(s->d_raw, tris, (size_t)n_tris * sizeof(rt2_triangle), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(s->d_mats, mats, (size_t)n_mats * sizeof(rt2_material), hipMemcpyHostToDevice));
+    if (s->n_nodes > 0) {
+        HIPCHECK(hipMalloc(&s->d_nodes, (size_t)n_nodes * sizeof(rt2_node)));
+        HIPCHECK(hipMemcpy(s->d_nodes, nodes, (size_t)n_nodes * sizeof(rt2_node), hipMemcpyHostToDevice));
+    }
+    if (n_tris > 0) {
+        hipLaunchKernelGGL(prep_triangles, dim3((n_tris + 255) / 256), dim3(256), 0, 0, s->d_raw, n_tris, s->d_tri,
+                           s->d_mtl);
+        HIPCHECK(hipGetLastError());
+    }
+    HIPCHECK(hipDeviceSynchronize());
+    *out = s;
+    return 0;
+}
+
+extern "C" void rt2_scene_destroy(rt2_scene* s) {
+    if (!s) return;
+    (void)hipSetDevice(s->device);
+    (void)hipFree(s->d_raw);
+    (void)hipFree(s->d_tri);
+    (void)hipFree(s->d_mtl);
+    (void)hipFree(s->d_mats);
+    (void)hipFree(s->d_nodes);
+    (void)hipFree(s->d_counters);
+    delete s;
+}
+
+extern "C" int32_t rt2_shard_rows(int32_t height, rt2_shard sh) {
+    if (sh.tile_rows < 1 || sh.nranks < 1 || sh.rank < 0 || sh.rank >= sh.nranks || height < 0) return -1;
+    int32_t n = 0;
+    for (int32_t t = sh.rank; (int64_t)t * sh.tile_rows < height; t += sh.nranks)
+        n += std::min(sh.tile_rows, height - t * sh.tile_rows);
+    return n;
+}
+
+extern "C" int32_t rt2_shard_row(int32_t local_row, rt2_shard sh) {
+    int32_t t = local_row / sh.tile_rows;
+    return (t * sh.nranks + sh.rank) * sh.tile_rows + local_row % sh.tile_rows;
+}
+
+extern "C" int rt2_scene_set_variant(rt2_scene* s, int variant) {
+    if (!s) return -1;
+    s->variant = variant;
+    return variant;
+}
+
+namespace {
+constexpr int kBlockResident = 256;
+constexpr int kBlockTiled = 256;
+constexpr int kTileTris = 1024;  // 48 KiB of LDS per tile
+}  // namespace
+
+extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_begin, uint32_t frame_count,
+                          rt2_shard sh, float* d_accum, uint32_t* d_accum8, void* stream) {
+    if (!s || !u || !d_accum) {
+        rt2h::set_error("rt2_render: null argument");
+        return -1;
+    }
+    if (u->basicShading) {
+        rt2h::set_error("rt2_render: basicShading (traceBasic preview) is not on this path");
+        return -1;
+    }
+    if (u->numRaysPerPixel < 1 || u->width < 1 || u->height < 1) {
+        rt2h::set_error("rt2_render: numRaysPerPixel, width and height must be >= 1");
+        return -1;
+    }
+    const int rows = rt2_shard_rows((int)u->height, sh);
+    if (rows < 0) {
+        rt2h::set_error("rt2_render: bad shard");
+        return -1;
+    }
+    if (frame_count == 0 || rows == 0) return 0;
+    HIPCHECK(hipSetDevice(s->device));
+    hipStream_t st = (hipStream_t)stream;
+
+    RenderParams p;
+    std::memset(&p, 0, sizeof(p));
+    p.tri = s->d_tri;
+    p.tri_mtl = s->d_mtl;
+    p.mats = s->d_mats;
+    p.n_tris = s->n_tris;
+    p.n_mats = s->n_mats;
+    p.W = (int)u->width;
+    p.H = (int)u->height;
+    p.maxBounce = u->maxBounceCount;
+    p.R = u->numRaysPerPixel;
+    p.envLight = u->environmentalLight;
+    auto cp = [](float* d, const rt2_vec4& v) {
+        d[0] = v.x;
+        d[1] = v.y;
+        d[2] = v.z;
+    };
+    cp(p.cam, u->cameraPos);
+    cp(p.vpRight, u->viewportRight);
+    cp(p.vpUp, u->viewportUp);
+    cp(p.vpFront, u->viewportFront);
+    cp(p.pixR, u->pixelRight);
+    cp(p.pixU, u->pixelUp);
+    cp(p.defR, u->defocusDiskRight);
+    cp(p.defU, u->defocusDiskUp);
+    p.frame_begin = frame_begin;
+    p.frame_count = frame_count;
+    p.tile_rows = sh.tile_rows;
+    p.rank = sh.rank;
+    p.nranks = sh.nranks;
+    p.n_items = (unsigned long long)rows * (unsigned long long)p.W;
+    p.accum = reinterpret_cast<float4*>(d_accum);
+    p.accum8 = reinterpret_cast<uint4*>(d_accum8);
+    p.item_counter = s->d_counters;
+    p.seg_counter = s->d_counters + 1;
+    p.tile_tris = kTileTris;
+
+    HIPCHECK(hipMemsetAsync(s->d_counters, 0, sizeof(unsigned long long), st));
+    const size_t resident_bytes = (size_t)3 * sizeof(float4) * (size_t)std::max(s->n_tris, 1);
+    const bool resident = (s->variant == 0 || s->variant == 1) && resident_bytes <= 96 * 1024 && s->variant != 2;
+    if (resident) {
+        int occ = 0;
+        HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, render_resident<kBlockResident>, kBlockResident,
+                                                              resident_bytes));
+        occ = std::max(occ, 1);
+        const unsigned long long waves_needed = (p.n_items + kWave - 1) / kWave;
+        unsigned long long blocks = (unsigned long long)s->num_cus * occ;
+        blocks = std::min(blocks, (waves_needed * kWave + kBlockResident - 1) / kBlockResident);
+        blocks = std::max(blocks, 1ull);
+        hipLaunchKernelGGL(render_resident<kBlockResident>, dim3((unsigned)blocks), dim3(kBlockResident),
+                           resident_bytes, st, p);
+    } else {
+        const size_t tile_bytes = (size_t)3 * sizeof(float4) * kTileTris;
+        int occ = 0;
+        HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, render_tiled<kBlockTiled>, kBlockTiled, tile_bytes));
+        occ = std::max(occ, 1);
+        unsigned long long blocks = (unsigned long long)s->num_cus * occ;
+        blocks = std::min(blocks, (p.n_items + kBlockTiled - 1) / kBlockTiled);
+        blocks = std::max(blocks, 1ull);
+        hipLaunchKernelGGL(render_tiled<kBlockTiled>, dim3((unsigned)blocks), dim3(kBlockTiled), tile_bytes, st, p);
+    }
+    HIPCHECK(hipGetLastError());
+    s->samples += p.n_items * (unsigned long long)p.R * (unsigned long long)frame_count;
+    s->tests_per_seg = (unsigned long long)s->n_tris;
+    return 0;
+}
+
+extern "C" int rt2_scene_stats(rt2_scene* s, rt2_stats* out, int reset) {
+    if (!s || !out) {
+        rt2h::set_error("rt2_scene_stats: null argument");
+        return -1;
+    }
+    HIPCHECK(hipSetDevice(s->device));
+    HIPCHECK(hipDeviceSynchronize());
+    unsigned long long c[4];
+    HIPCHECK(hipMemcpy(c, s->d_counters, sizeof(c), hipMemcpyDeviceToHost));
+    out->samples = s->samples;
+    out->segments = c[1];
+    out->tests = c[1] * (unsigned long long)s->n_tris;
+    if (reset) {
+        s->samples = 0;
+        HIPCHECK(hipMemset(s->d_counters, 0, sizeof(c)));
+    }
+    return 0;
+}
+
+extern "C" int rt2_resolve_rgba32f(const float* d_accum, int64_t n, uint32_t frames, float* d_out, void* stream) {
+    if (!d_accum || !d_out || n < 0 || frames == 0) {
+        rt2h::set_error("rt2_resolve_rgba32f: bad argument");
+        return -1;
+    }
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(resolve_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const float4*>(d_accum), (long long)n, 0.0f, (float)frames,
+                       reinterpret_cast<float4*>(d_out));
+    HIPCHECK(hipGetLastError());
+    return 0;
+}
+
+extern "C" int rt2_resolve_rgb8_reference(const uint32_t* acc8, int64_t n, uint32_t frames, uint8_t* out) {
+    if (!acc8 || !out || n < 0 || frames == 0) {
+        rt2h::set_error("rt2_resolve_rgb8_reference: bad argument");
+        return -1;
+    }
+    const float F = (float)frames;
+    for (int64_t i = 0; i < n; i++)
+        for (int c = 0; c < 3; c++) {
+            float v = std::min(255.0f, (float)acc8[4 * i + c] / F);
+            out[3 * i + c] = (uint8_t)v;
+        }
+    return 0;
+}
+
+extern "C" int rt2_render_host(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_begin, uint32_t frame_count,
+                               rt2_shard sh, float* out_rgba, uint8_t* out_rgb8) {
+    if (!s || !u) {
+        rt2h::set_error("rt2_render_host: null argument");
+        return -1;
+    }
+    const int rows = rt2_shard_rows((int)u->height, sh);
+    if (rows < 0) {
+        rt2h::set_error("rt2_render_host: bad shard");
+        return -1;
+    }
+    const size_t n = (size_t)rows * u->width;
+    HIPCHECK(hipSetDevice(s->device));
+    float* acc = nullptr;
+    float* res = nullptr;
+    uint32_t* acc8 = nullptr;
+    HIPCHECK(hipMalloc(&acc, std::max(n, (size_t)1) * 16));
+    HIPCHECK(hipMalloc(&res, std::max(n, (size_t)1) * 16));
+    HIPCHECK(hipMemset(acc, 0, std::max(n, (size_t)1) * 16));
+    if (out_rgb8) {
+        HIPCHECK(hipMalloc(&acc8, std::max(n, (size_t)1) * 16));
+        HIPCHECK(hipMemset(acc8, 0, std::max(n, (size_t)1) * 16));
+    }
+    int rc = rt2_render(s, u, frame_begin, frame_count, sh, acc, acc8, nullptr);
+    if (rc == 0 && out_rgba && n) {
+        rc = rt2_resolve_rgba32f(acc, (int64_t)n, frame_count, res, nullptr);
+        if (rc == 0) {
+            hipError_t e = hipMemcpy(out_rgba, res, n * 16, hipMemcpyDeviceToHost);
+            if (e != hipSuccess) {
+                rt2h::set_error(std::string("hipMemcpy: ") + hipGetErrorString(e));
+                rc = -1;
+            }
+        }
+    }
+    if (rc == 0 && out_rgb8 && n) {
+        std::vector<uint32_t> h8(n * 4);
+        hipError_t e = hipMemcpy(h8.data(), acc8, n * 16, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) {
+            rt2h::set_error(std::string("hipMemcpy: ") + hipGetErrorString(e));
+            rc = -1;
+        } else {
+            rc = rt2_resolve_rgb8_reference(h8.data(), (int64_t)n, frame_count, out_rgb8);
+        }
+    }
+    hipError_t e = hipDeviceSynchronize();
+    if (rc == 0 && e != hipSuccess) {
+        rt2h::set_error(std::string("render: ") + hipGetErrorString(e));
+        rc = -1;
+    }
+    (void)hipFree(acc);
+    (void)hipFree(res);
+    (void)hipFree(acc8);
+    return rc;
+}
+
+// Not in rt2.h (test hook): device numerics self-test, host in/out arrays.
+extern "C" int rt2_device_selftest(const float* in, int32_t n, float* out10) {
+    float *din = nullptr, *dout = nullptr;
+    HIPCHECK(hipMalloc(&din, (size_t)n * 4));
+    HIPCHECK(hipMalloc(&dout, (size_t)n * 40));
+    HIPCHECK(hipMemcpy(din, in, (size_t)n * 4, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(selftest_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, din, n, dout);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipMemcpy(out10, dout, (size_t)n * 40, hipMemcpyDeviceToHost));
+    (void)hipFree(din);
+    (void)hipFree(dout);
+    return 0;
+}
