@@ -386,11 +386,16 @@ static void* worker(void* arg) {
     const ctx_t* c = j->c;
     int W = (int)c->u->width;
     uint64_t segs = 0, tests = 0;
+    const int chunk = 32; /* work unit: 32 pixels of one row */
+    const int per_row = (W + chunk - 1) / chunk;
     for (;;) {
-        int r = atomic_fetch_add(&j->next_row, 1);
-        if (r >= j->n_rows) break;
+        int unit = atomic_fetch_add(&j->next_row, 1);
+        if (unit >= j->n_rows * per_row) break;
+        int r = unit / per_row;
         int ty = j->rows[r];
-        for (int tx = 0; tx < W; tx++) {
+        int x0 = (unit % per_row) * chunk;
+        int x1 = x0 + chunk < W ? x0 + chunk : W;
+        for (int tx = x0; tx < x1; tx++) {
             float acc[3] = {0.0f, 0.0f, 0.0f};
             uint32_t a8[3] = {0, 0, 0};
             for (uint32_t f = 0; f < j->frame_count; f++) {

@@ -44,6 +44,26 @@ __device__ __forceinline__ float smoothstep(float e0, float e1, float x) {
     return t * t * (3.0f - 2.0f * t);
 }
 
+// Reciprocal sequences built on v_rcp_f32 (<= 1 ulp) + FMA Newton/quotient
+// refinement (the f32 fdiv expansion of the AMDGPU backend without its
+// div_scale/div_fixup range handling).  rcp_variant(x, 3) is bit-identical to
+// IEEE 1.0f/x for every x whose reciprocal is a normal number — checked
+// exhaustively on the device over all such bit patterns
+// (tests/test_gpu_numerics.py::test_rcp_exhaustive).
+__device__ __forceinline__ float rcp_variant(float x, int v) {
+    float r = __builtin_amdgcn_rcpf(x);
+    if (v == 0) return r;
+    float e = __builtin_fmaf(-x, r, 1.0f);
+    r = __builtin_fmaf(e, r, r);
+    if (v == 1) return r;
+    float q = r;
+    float rem = __builtin_fmaf(-x, q, 1.0f);
+    q = __builtin_fmaf(rem, r, q);
+    if (v == 2) return q;
+    rem = __builtin_fmaf(-x, q, 1.0f);
+    return __builtin_fmaf(rem, r, q);
+}
+
 // random, compute.glsl:148-154 — PCG-RXS-M-XS, result / 2^32
 __device__ __forceinline__ float rnd(uint32_t& state) {
     state = state * 747796405u + 2891336453u;

@@ -405,6 +405,27 @@ __global__ void selftest_kernel(const float* in, int n, float* out) {
     out[10 * i + 9] = 1.0f / x;
 }
 
+// Exhaustive check of the reciprocal sequences against IEEE 1.0f / x over a
+// range of float bit patterns (test hook for the division-free exact path).
+__global__ void rcp_check_kernel(uint32_t lo, unsigned long long count, int variant,
+                                 unsigned long long* mismatches, uint32_t* first_bad) {
+    unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+    unsigned long long bad = 0;
+    for (; i < count; i += stride) {
+        const uint32_t bits = lo + (uint32_t)i;
+        const float x = __uint_as_float(bits);
+        const float ref = 1.0f / x;
+        float r = rcp_variant(x, variant);
+        if (__float_as_uint(r) != __float_as_uint(ref)) {
+            bad++;
+            atomicMin(first_bad, bits);
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) bad += __shfl_xor(bad, off);
+    if ((threadIdx.x & 63) == 0 && bad) atomicAdd(mismatches, bad);
+}
+
 }  // namespace
 
 /* =========================================================================
@@ -716,6 +737,23 @@ extern "C" int rt2_render_host(rt2_scene* s, const rt2_uniforms* u, uint32_t fra
     (void)hipFree(res);
     (void)hipFree(acc8);
     return rc;
+}
+
+// Not in rt2.h (test hook): exhaustive reciprocal check over [lo, hi] bit patterns.
+extern "C" int rt2_device_rcp_check(uint32_t lo, uint32_t hi, int variant, unsigned long long* mismatches,
+                                    uint32_t* first_bad) {
+    unsigned long long* d = nullptr;
+    HIPCHECK(hipMalloc(&d, 16));
+    HIPCHECK(hipMemset(d, 0, 8));
+    uint32_t init = 0xffffffffu;
+    HIPCHECK(hipMemcpy((char*)d + 8, &init, 4, hipMemcpyHostToDevice));
+    const unsigned long long count = (unsigned long long)hi - lo + 1;
+    hipLaunchKernelGGL(rcp_check_kernel, dim3(4096), dim3(256), 0, 0, lo, count, variant, d, (uint32_t*)((char*)d + 8));
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipMemcpy(mismatches, d, 8, hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(first_bad, (char*)d + 8, 4, hipMemcpyDeviceToHost));
+    (void)hipFree(d);
+    return 0;
 }
 
 // Not in rt2.h (test hook): device numerics self-test, host in/out arrays.

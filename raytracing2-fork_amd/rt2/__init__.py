@@ -165,6 +165,17 @@ def lib() -> C.CDLL:
     if not os.path.exists(LIB_PATH):
         raise RT2Error(f"{LIB_PATH} is missing: build it with `make -C raytracing2-fork_amd` "
                        "(or __graft_entry__.build()); the render path has no CPU fallback")
+    # One HIP runtime per process.  torch ships its own libamdhip64 (SONAME
+    # libamdhip64.so.7, but its libs NEED the file name "libamdhip64.so"): if
+    # librt2 loaded /opt/rocm's runtime first, importing torch afterwards would
+    # bring a second runtime and the two would fight over the device.  Loading
+    # torch first makes librt2's NEEDED libamdhip64.so.7 bind to torch's copy,
+    # so torch tensors and rt2 kernels share one runtime (and one context).
+    if os.environ.get("RT2_NO_TORCH", "0") != "1":
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     L = C.CDLL(LIB_PATH)
     P, I32, U32, I64, F = C.c_void_p, C.c_int32, C.c_uint32, C.c_int64, C.c_float
     sig = {

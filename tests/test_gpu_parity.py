@@ -1,0 +1,236 @@
+"""GPU parity: the HIP render path (through the C-ABI) against the CPU oracle.
+
+Bar: bit-exact.  Both sides evaluate the pinned arithmetic of DESIGN.md
+§Numerics (IEEE f32, explicit fma in dot/cross, pinned transcendentals), so a
+pixel either matches in every bit or the implementation has a bug.  The
+north-star tolerance (per-pixel RMSE < 1e-4) is asserted as well, as the
+outer bound.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+RMSE_TOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch  # loads torch's HIP runtime first: librt2 then shares it
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    torch.cuda.set_device(0)
+    return torch
+
+
+def oracle_mean(oraclemod, sd, u, rows, fb, fc, mode="brute", tris=None, mats=None):
+    acc, acc8, segs, tests = oraclemod.render(sd.triangles() if tris is None else tris,
+                                              sd.materials() if mats is None else mats, u, rows, fb, fc, mode,
+                                              nodes=sd.nodes() if mode == "bvh" else None, with_acc8=True)
+    return acc[..., :3] / np.float32(fc), acc8, segs
+
+
+def assert_exact(gpu, ref, what=""):
+    d = np.abs(gpu[..., :3].astype(np.float64) - ref[..., :3].astype(np.float64))
+    rmse = float(np.sqrt((d ** 2).mean())) if d.size else 0.0
+    assert rmse < RMSE_TOL, f"{what}: rmse {rmse}"
+    bad = (d.max(-1) > 0)
+    assert not bad.any(), f"{what}: {bad.sum()} of {bad.size} pixels differ, max {d.max():.3e}, rmse {rmse:.3e}"
+
+
+def test_device_numerics(rt2mod, oraclemod, torch_cuda):
+    rng = np.random.default_rng(0)
+    x = np.concatenate([rng.uniform(-20, 20, 3000), rng.uniform(-1, 1, 1000),
+                        np.exp(rng.uniform(-80, 80, 1000)) * rng.choice([-1, 1], 1000)]).astype(np.float32)
+    n = len(x)
+    out = rt2mod.device_selftest(x)
+    y = x[(np.arange(n) * 7 + 3) % n]
+    with np.errstate(all="ignore"):
+        assert np.array_equal(out[:, 0], x / y, equal_nan=True)
+        assert np.array_equal(out[:, 1], np.sqrt(np.abs(x)))
+        assert np.array_equal(out[:, 9], np.float32(1.0) / x)
+        fma = (x.astype(np.float64) * y.astype(np.float64) + x.astype(np.float64)).astype(np.float32)
+    # float64 product+sum then one rounding == fma except double-rounding corner cases
+    assert (out[:, 2] == fma).mean() > 0.999
+    for col, k, arg in ((3, 0, x), (4, 1, np.abs(x)), (5, 2, np.clip(y, -1, 1)), (6, 3, x), (7, 4, x)):
+        host = np.array([oraclemod.pinned(k, float(v)) for v in arg], np.float32)
+        assert np.array_equal(out[:, col], host, equal_nan=True), (col, k)
+
+
+def test_config_A_full_frame_exact(rt2mod, oraclemod, config_scene, torch_cuda):
+    sd, spec = config_scene("A")
+    u = rt2mod.offline_uniforms(spec.width, spec.height, spec.bounces, spec.rays, sd.num_triangles)
+    scene = rt2mod.Scene(sd, 0)
+    img = scene.render_host(u, 0, spec.frames)
+    st = scene.stats(reset=True)
+    ref, _, segs = oracle_mean(oraclemod, sd, u, np.arange(spec.height), 0, spec.frames)
+    assert_exact(img, ref, "config A")
+    assert st.segments == segs
+    assert st.samples == spec.width * spec.height * spec.rays * spec.frames
+
+
+def test_config_B_full_size_rows_exact(rt2mod, oraclemod, config_scene, torch_cuda):
+    """Config B at its full size (1920x1080, 64 rays, 8 bounces); strided rows vs the oracle."""
+    sd, spec = config_scene("B")
+    u = rt2mod.offline_uniforms(spec.width, spec.height, spec.bounces, spec.rays, sd.num_triangles)
+    scene = rt2mod.Scene(sd, 0)
+    img = scene.render_host(u, 0, spec.frames)
+    assert img.shape == (1080, 1920, 4)
+    assert np.all(img[..., 3] == 1.0)
+    assert np.isfinite(img).all() and (img[..., :3] >= 0).all() and (img[..., :3] <= 1).all()
+    rows = np.array([0, 1, 539, 540, 1078, 1079], np.int32)
+    ref, _, _ = oracle_mean(oraclemod, sd, u, rows, 0, spec.frames, "brute")
+    assert_exact(img[rows], ref, "config B brute rows")
+    rows = np.arange(5, 1080, 45, dtype=np.int32)
+    ref, _, _ = oracle_mean(oraclemod, sd, u, rows, 0, spec.frames, "bvh")
+    # BVH traversal equals brute force except on exact distance ties
+    d = np.abs(img[rows][..., :3] - ref)
+    assert (d.max(-1) == 0).mean() > 0.999
+    assert np.sqrt((d ** 2).mean()) < RMSE_TOL
+
+
+def test_frames_split_across_calls_bit_identical(rt2mod, config_scene, torch_cuda):
+    torch = torch_cuda
+    sd, spec = config_scene("A")
+    W, H = 64, 40
+    u = rt2mod.offline_uniforms(W, H, 4, 3, sd.num_triangles)
+    scene = rt2mod.Scene(sd, 0)
+    sh = rt2mod.shard()
+    a = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+    b = torch.zeros_like(a)
+    a8 = torch.zeros((H, W, 4), dtype=torch.int32, device="cuda")
+    b8 = torch.zeros_like(a8)
+    scene.render(u, 5, 4, sh, a.data_ptr(), a8.data_ptr())
+    for fb, fc in ((5, 1), (6, 2), (8, 1)):
+        scene.render(u, fb, fc, sh, b.data_ptr(), b8.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(a, b) and torch.equal(a8, b8)
+
+
+def test_shards_assemble_to_full_image(rt2mod, config_scene, torch_cuda):
+    sd, spec = config_scene("A")
+    W, H = 96, 61
+    u = rt2mod.offline_uniforms(W, H, 4, 2, sd.num_triangles)
+    scene = rt2mod.Scene(sd, 0)
+    full = scene.render_host(u, 0, 2)
+    for tile, n in ((1, 2), (8, 3), (4, 8)):
+        img = np.zeros_like(full)
+        for r in range(n):
+            sh = rt2mod.shard(tile, r, n)
+            slab = scene.render_host(u, 0, 2, sh)
+            img[rt2mod.shard_row_ids(H, sh)] = slab
+        assert np.array_equal(img, full), (tile, n)
+
+
+def test_rgb8_reference_path(rt2mod, oraclemod, config_scene, torch_cuda):
+    sd, spec = config_scene("A")
+    W, H, F = 80, 50, 3
+    u = rt2mod.offline_uniforms(W, H, 4, 2, sd.num_triangles)
+    scene = rt2mod.Scene(sd, 0)
+    img, rgb8 = scene.render_host(u, 0, F, rgb8=True)
+    ref, acc8, _ = oracle_mean(oraclemod, sd, u, np.arange(H), 0, F)
+    assert_exact(img, ref)
+    expect = np.minimum(255.0, acc8[..., :3].astype(np.float32) / np.float32(F)).astype(np.uint8)
+    assert np.array_equal(rgb8, expect)
+
+
+@pytest.mark.parametrize("W,H,R,B", [(37, 13, 1, 8), (17, 9, 3, 0), (33, 7, 2, 1), (1, 1, 5, 20)])
+def test_odd_sizes_and_bounce_limits(rt2mod, oraclemod, config_scene, torch_cuda, W, H, R, B):
+    sd, spec = config_scene("A")
+    u = rt2mod.offline_uniforms(W, H, B, R, sd.num_triangles)
+    scene = rt2mod.Scene(sd, 0)
+    img = scene.render_host(u, 3, 2)
+    ref, _, segs = oracle_mean(oraclemod, sd, u, np.arange(H), 3, 2)
+    assert_exact(img, ref, f"{W}x{H} R{R} B{B}")
+    assert scene.stats().segments == segs
+    if B == 0:
+        assert np.all(img[..., :3] == 0)
+
+
+def test_diverse_materials_exact(rt2mod, oraclemod, torch_cuda):
+    """Glass, checker, mirror and glossy-specular materials (compute.glsl:499-546)."""
+    M = rt2mod.Material
+    sd = rt2mod.SceneData()
+    red = sd.add_material(M.diffuse((1, 0, 0)))
+    green = sd.add_material(M.diffuse((0, 1, 0)))
+    white = sd.add_material(M.diffuse((1, 1, 1)))
+    light = sd.add_material(M.light((1, 1, 1), 15.0))
+    glass = sd.add_material(M.glass((0.9, 0.95, 1.0), 1.5))
+    mirror = sd.add_material(M.specular((1, 1, 1), (1, 1, 1), 1.0, 1.0))
+    checker = sd.add_material(M.checker(8.0))
+    metal = sd.add_material(M.specular((0.8, 0.6, 0.3), (1, 1, 1), 0.7, 0.4))
+    edge = M.diffuse((0.5, 0.5, 0.9))
+    edge.isEdgeHighlight = 1
+    sd.add_material(edge)
+    sd.create_diverse_cornell_box(10.0, red, green, white, light, glass, mirror, checker, metal)
+    sd.add_cube((0.0, -2.0, 0.0), (1.0, 1.0, 1.0), (0.3, 0.2, 0.1), 8)
+    sd.build_bvh()
+    W, H = 96, 64
+    u = rt2mod.offline_uniforms(W, H, 12, 4, sd.num_triangles)
+    scene = rt2mod.Scene(sd, 0)
+    img = scene.render_host(u, 0, 2)
+    ref, _, segs = oracle_mean(oraclemod, sd, u, np.arange(H), 0, 2)
+    assert_exact(img, ref, "diverse")
+    assert scene.stats().segments == segs
+
+
+def test_defocus_and_frame_wrap(rt2mod, oraclemod, config_scene, torch_cuda):
+    """Non-zero defocus exercises cos/sin of randomDirection2D; frame indices near
+    2^32 exercise the uint32 seed wrap (compute.glsl:668)."""
+    sd, spec = config_scene("A")
+    cam = rt2mod.default_camera(48, 32)
+    cam.defocus_angle = 0.05
+    u = rt2mod.offline_uniforms(48, 32, 6, 3, sd.num_triangles)
+    rt2mod.camera_uniforms(cam, u)
+    assert u.defocusDiskRight.x != 0
+    scene = rt2mod.Scene(sd, 0)
+    fb = 2**32 - 2
+    img = scene.render_host(u, fb, 3)
+    ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(32), fb, 3)
+    assert_exact(img, ref, "defocus + wrap")
+
+
+def test_tiled_kernel_exact(rt2mod, oraclemod, config_scene, torch_cuda):
+    """The LDS-tiled sweep (forced on a small scene, and automatic on 100k triangles)."""
+    sd, spec = config_scene("B")
+    u = rt2mod.offline_uniforms(96, 54, 8, 4, sd.num_triangles)
+    scene = rt2mod.Scene(sd, 0)
+    scene.set_variant(2)
+    img = scene.render_host(u, 0, 1)
+    ref, _, segs = oracle_mean(oraclemod, sd, u, np.arange(54), 0, 1)
+    assert_exact(img, ref, "tiled B")
+    assert scene.stats().segments == segs
+    sdc, specc = config_scene("C")
+    assert sdc.num_triangles == 100016
+    u = rt2mod.offline_uniforms(24, 14, 8, 2, sdc.num_triangles)
+    scene = rt2mod.Scene(sdc, 0)
+    img = scene.render_host(u, 0, 1)
+    ref, _, _ = oracle_mean(oraclemod, sdc, u, np.arange(14), 0, 1, "bvh")
+    d = np.abs(img[..., :3] - ref)
+    assert (d.max(-1) == 0).mean() > 0.99 and np.sqrt((d ** 2).mean()) < RMSE_TOL
+
+
+def test_empty_and_single_triangle_scenes(rt2mod, oraclemod, torch_cuda):
+    M = rt2mod.Material
+    sd = rt2mod.SceneData()
+    sd.add_material(M.diffuse((0.7, 0.7, 0.7)))
+    u = rt2mod.offline_uniforms(20, 10, 4, 2, 0)
+    scene = rt2mod.Scene(sd, 0)
+    img = scene.render_host(u, 0, 1)
+    ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(10), 0, 1)
+    assert_exact(img, ref, "empty scene (sky only)")
+    sd.add_triangle((-3, 0, -2), (3, 0, -2), (0, 8, -2), 0)
+    u = rt2mod.offline_uniforms(20, 10, 4, 2, 1)
+    scene = rt2mod.Scene(sd, 0)
+    img = scene.render_host(u, 0, 1)
+    ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(10), 0, 1)
+    assert_exact(img, ref, "one triangle")
+
+
+def test_bad_material_index_rejected(rt2mod, torch_cuda):
+    sd = rt2mod.SceneData()
+    sd.add_material(rt2mod.Material.default())
+    sd.add_triangle((0, 0, 0), (1, 0, 0), (0, 1, 0), 5)
+    with pytest.raises(rt2mod.RT2Error, match="material index"):
+        rt2mod.Scene(sd, 0)
