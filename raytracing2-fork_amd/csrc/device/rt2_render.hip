@@ -37,7 +37,6 @@ using namespace rt2d;
 
 namespace {
 
-constexpr int kWave = 64;
 
 struct RenderParams {
     const float4* tri;  // 3 float4 per triangle: {ax ay az e0x} {e0y e0z e1x e1y} {e1z nx ny nz}
@@ -95,6 +94,63 @@ __device__ __forceinline__ void mt_test(const f3& o, const f3& d, float4 t0, flo
         best = dst;
         best_i = idx;
     }
+}
+
+// Filtered Möller–Trumbore: same decision as mt_test, bit for bit.
+//
+// With det = -dot(d,n), inv = RN(1/det), the reference updates the closest hit
+// iff det >= 1e-10, dst = RN(tnum*inv) > 1e-6, u = RN(-U*inv) >= 0,
+// v = RN(V*inv) >= 0, RN(RN(1-u)-v) >= 0 and dst < best, where tnum =
+// dot(o-a, n), U = dot(e1, q), V = dot(e0, q), q = cross(d, o-a).  The filter
+// F below uses only those exact intermediates (no division) and is false only
+// when the update is impossible ("Exactness of the
+// filter"): for det > 0, inv > 0, so
+//   tnum <= 0                      => dst <= 0                (reject)
+//   U > det*2^-60                  => u <= -2^-61 < 0         (reject)
+//   V < -det*2^-60                 => v < 0                   (reject)
+//   RN(V-U) > RN(det*(1+2^-10))    => w < 0 (u, v >= -2^-60)  (reject)
+//   tnum > RN(det*RN(best*(1+2^-10))) => dst >= best          (no update)
+// det < 0, det = 0 and NaN fail `tnum > 0 && tnum <= det*bestK`; 0 < det <
+// 1e-10 and det = +inf pass F and are rejected by the exact path, as in the
+// reference.  Only F-survivors (a few per mille of pairs) pay for the IEEE
+// division.
+__device__ __forceinline__ void mt_test_filtered(const f3& o, const f3& d, float4 t0, float4 t1, float4 t2, int idx,
+                                                 float& best, int& best_i, float& bestK) {
+    const f3 a = mk(t0.x, t0.y, t0.z);
+    const f3 e0 = mk(t0.w, t1.x, t1.y);
+    const f3 e1 = mk(t1.z, t1.w, t2.x);
+    const f3 n = mk(t2.y, t2.z, t2.w);
+    const float det = -dot(d, n);
+    const f3 ao = sub(o, a);
+    const float tnum = dot(ao, n);
+    const f3 q = cross(d, ao);
+    const float U = dot(e1, q);
+    const float V = dot(e0, q);
+    const float B = det * 0x1p-60f;
+    const bool F = (tnum > 0.0f) & (U <= B) & (V >= -B) & ((V - U) <= det * 1.0009765625f) & (tnum <= det * bestK);
+    if (F) {
+        // compute.glsl:312-327, exactly as written
+        if (!((det < 1e-10f && det > -1e-10f) || det < 0.0f)) {
+            const float inv = 1.0f / det;
+            const float dst = tnum * inv;
+            const float u = -U * inv;
+            const float v = V * inv;
+            if (!(dst <= 1e-6f) && !(u < 0.0f || v < 0.0f || 1.0f - u - v < 0.0f) && dst < best) {
+                best = dst;
+                best_i = idx;
+                bestK = best * 1.0009765625f;
+            }
+        }
+    }
+}
+
+template <int MT>
+__device__ __forceinline__ void mt_dispatch(const f3& o, const f3& d, float4 t0, float4 t1, float4 t2, int idx,
+                                            float& best, int& best_i, float& bestK) {
+    if constexpr (MT == 0)
+        mt_test(o, d, t0, t1, t2, idx, best, best_i);
+    else
+        mt_test_filtered(o, d, t0, t1, t2, idx, best, best_i, bestK);
 }
 
 struct Lane {
@@ -298,7 +354,7 @@ __device__ __forceinline__ void flush_counters(const Lane& L, const RenderParams
 }
 
 // RESIDENT: all triangles in LDS, waves independent after the initial load.
-template <int BLOCK>
+template <int BLOCK, int MT, int UNROLL>
 __global__ __launch_bounds__(BLOCK) void render_resident(RenderParams p) {
     extern __shared__ float4 lds[];
     const int n4 = 3 * p.n_tris;
@@ -313,12 +369,12 @@ __global__ __launch_bounds__(BLOCK) void render_resident(RenderParams p) {
         if (L.st == ST_TRACE) {
             L.bounce += 1;
             L.segs += 1;
-            float best = 1e38f;
+            float best = 1e38f, bestK = 1e38f * 1.0009765625f;
             int bi = -1;
             const f3 o = L.o, d = L.d;
-#pragma unroll 4
+#pragma unroll UNROLL
             for (int i = 0; i < p.n_tris; i++) {
-                mt_test(o, d, lds[3 * i], lds[3 * i + 1], lds[3 * i + 2], i, best, bi);
+                mt_dispatch<MT>(o, d, lds[3 * i], lds[3 * i + 1], lds[3 * i + 2], i, best, bi, bestK);
             }
             shade(L, p, best, bi);
         }
@@ -327,7 +383,7 @@ __global__ __launch_bounds__(BLOCK) void render_resident(RenderParams p) {
 }
 
 // TILED: triangles streamed through LDS; the workgroup sweeps in lockstep.
-template <int BLOCK>
+template <int BLOCK, int MT, int UNROLL>
 __global__ __launch_bounds__(BLOCK) void render_tiled(RenderParams p) {
     extern __shared__ float4 lds[];
     __shared__ int block_any;
@@ -342,7 +398,7 @@ __global__ __launch_bounds__(BLOCK) void render_tiled(RenderParams p) {
         __syncthreads();
         if (!block_any) break;
         const bool tracing = L.st == ST_TRACE;
-        float best = 1e38f;
+        float best = 1e38f, bestK = 1e38f * 1.0009765625f;
         int bi = -1;
         const f3 o = L.o, d = L.d;
         for (int base = 0; base < p.n_tris; base += T) {
@@ -351,8 +407,9 @@ __global__ __launch_bounds__(BLOCK) void render_tiled(RenderParams p) {
             for (int i = threadIdx.x; i < 3 * cnt; i += BLOCK) lds[i] = p.tri[3 * base + i];
             __syncthreads();
             if (tracing) {
-#pragma unroll 4
-                for (int i = 0; i < cnt; i++) mt_test(o, d, lds[3 * i], lds[3 * i + 1], lds[3 * i + 2], base + i, best, bi);
+#pragma unroll UNROLL
+                for (int i = 0; i < cnt; i++)
+                    mt_dispatch<MT>(o, d, lds[3 * i], lds[3 * i + 1], lds[3 * i + 2], base + i, best, bi, bestK);
             }
         }
         if (tracing) {
@@ -455,6 +512,7 @@ struct rt2_scene {
     unsigned long long* d_counters = nullptr;  // [0] item counter, [1] segments
     unsigned long long samples = 0, tests_per_seg = 0;
     int variant = 0;
+    int last_variant = -1;
     int num_cus = 256;
     size_t max_lds = 65536;
 };
@@ -543,10 +601,50 @@ extern "C" int rt2_scene_set_variant(rt2_scene* s, int variant) {
 }
 
 namespace {
-constexpr int kBlockResident = 256;
-constexpr int kBlockTiled = 256;
 constexpr int kTileTris = 1024;  // 48 KiB of LDS per tile
+
+// Kernel variants (rt2_scene_set_variant); 0 = auto = the default below.
+struct Variant {
+    bool tiled;
+    int block;
+    hipError_t (*launch)(const RenderParams&, int blocks, size_t lds, hipStream_t st);
+    hipError_t (*occupancy)(int* occ, size_t lds);
+    const char* name;
+};
+
+template <bool TILED, int BLOCK, int MT, int UNROLL>
+hipError_t launch_t(const RenderParams& p, int blocks, size_t lds, hipStream_t st) {
+    if constexpr (TILED)
+        hipLaunchKernelGGL((render_tiled<BLOCK, MT, UNROLL>), dim3(blocks), dim3(BLOCK), lds, st, p);
+    else
+        hipLaunchKernelGGL((render_resident<BLOCK, MT, UNROLL>), dim3(blocks), dim3(BLOCK), lds, st, p);
+    return hipGetLastError();
+}
+template <bool TILED, int BLOCK, int MT, int UNROLL>
+hipError_t occ_t(int* occ, size_t lds) {
+    if constexpr (TILED)
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_tiled<BLOCK, MT, UNROLL>, BLOCK, lds);
+    else
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_resident<BLOCK, MT, UNROLL>, BLOCK, lds);
+}
+#define RT2_VARIANT(T, B, M, U, NAME) Variant{T, B, launch_t<T, B, M, U>, occ_t<T, B, M, U>, NAME}
+
+const Variant kVariants[] = {
+    RT2_VARIANT(false, 512, 1, 4, "resident/512/filtered/u4"),   // 0: default (resident)
+    RT2_VARIANT(false, 256, 0, 4, "resident/256/plain/u4"),      // 1: round-1 v1 kernel
+    RT2_VARIANT(true, 256, 1, 4, "tiled/256/filtered/u4"),       // 2: default (tiled)
+    RT2_VARIANT(false, 256, 1, 4, "resident/256/filtered/u4"),   // 3
+    RT2_VARIANT(false, 1024, 1, 4, "resident/1024/filtered/u4"), // 4
+    RT2_VARIANT(false, 512, 1, 2, "resident/512/filtered/u2"),   // 5
+    RT2_VARIANT(false, 512, 1, 8, "resident/512/filtered/u8"),   // 6
+    RT2_VARIANT(true, 512, 1, 4, "tiled/512/filtered/u4"),       // 7
+    RT2_VARIANT(true, 1024, 1, 4, "tiled/1024/filtered/u4"),     // 8
+};
+constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+constexpr size_t kResidentMaxBytes = 112 * 1024;
 }  // namespace
+
+extern "C" const char* rt2_variant_name(int v) { return v >= 0 && v < kNumVariants ? kVariants[v].name : nullptr; }
 
 extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_begin, uint32_t frame_count,
                           rt2_shard sh, float* d_accum, uint32_t* d_accum8, void* stream) {
@@ -610,28 +708,20 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
 
     HIPCHECK(hipMemsetAsync(s->d_counters, 0, sizeof(unsigned long long), st));
     const size_t resident_bytes = (size_t)3 * sizeof(float4) * (size_t)std::max(s->n_tris, 1);
-    const bool resident = (s->variant == 0 || s->variant == 1) && resident_bytes <= 96 * 1024 && s->variant != 2;
-    if (resident) {
-        int occ = 0;
-        HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, render_resident<kBlockResident>, kBlockResident,
-                                                              resident_bytes));
-        occ = std::max(occ, 1);
-        const unsigned long long waves_needed = (p.n_items + kWave - 1) / kWave;
-        unsigned long long blocks = (unsigned long long)s->num_cus * occ;
-        blocks = std::min(blocks, (waves_needed * kWave + kBlockResident - 1) / kBlockResident);
-        blocks = std::max(blocks, 1ull);
-        hipLaunchKernelGGL(render_resident<kBlockResident>, dim3((unsigned)blocks), dim3(kBlockResident),
-                           resident_bytes, st, p);
-    } else {
-        const size_t tile_bytes = (size_t)3 * sizeof(float4) * kTileTris;
-        int occ = 0;
-        HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, render_tiled<kBlockTiled>, kBlockTiled, tile_bytes));
-        occ = std::max(occ, 1);
-        unsigned long long blocks = (unsigned long long)s->num_cus * occ;
-        blocks = std::min(blocks, (p.n_items + kBlockTiled - 1) / kBlockTiled);
-        blocks = std::max(blocks, 1ull);
-        hipLaunchKernelGGL(render_tiled<kBlockTiled>, dim3((unsigned)blocks), dim3(kBlockTiled), tile_bytes, st, p);
-    }
+    const bool fits = resident_bytes <= kResidentMaxBytes;
+    int vi = s->variant;
+    if (vi <= 0 || vi >= kNumVariants) vi = fits ? 0 : 2;
+    if (!kVariants[vi].tiled && !fits) vi = 2;  // a resident variant cannot hold this scene
+    const Variant& V = kVariants[vi];
+    const size_t lds = V.tiled ? (size_t)3 * sizeof(float4) * kTileTris : resident_bytes;
+    int occ = 0;
+    HIPCHECK(V.occupancy(&occ, lds));
+    occ = std::max(occ, 1);
+    unsigned long long blocks = (unsigned long long)s->num_cus * occ;
+    blocks = std::min(blocks, (p.n_items + V.block - 1) / V.block);
+    blocks = std::max(blocks, 1ull);
+    s->last_variant = vi;
+    HIPCHECK(V.launch(p, (int)blocks, lds, st));
     HIPCHECK(hipGetLastError());
     s->samples += p.n_items * (unsigned long long)p.R * (unsigned long long)frame_count;
     s->tests_per_seg = (unsigned long long)s->n_tris;

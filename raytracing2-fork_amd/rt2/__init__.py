@@ -225,6 +225,8 @@ def lib() -> C.CDLL:
         "rt2_uniforms_offline": (None, [C.POINTER(Uniforms), I32, I32, I32, I32, I32, I32]),
         "rt2_write_png": (C.c_int, [C.c_char_p, I32, I32, I32, P, I32]),
         "rt2_device_selftest": (C.c_int, [P, I32, P]),
+        "rt2_device_rcp_check": (C.c_int, [U32, U32, C.c_int, C.POINTER(C.c_ulonglong), C.POINTER(U32)]),
+        "rt2_variant_name": (C.c_char_p, [C.c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -1,0 +1,52 @@
+"""A/B of kernel variants in ONE process, interleaved rounds (cdna guide §5.4 rule 24).
+Renders a configuration with each variant, checks every variant's image is
+bit-identical to variant 1 (the round-1 kernel), reports median / min ms."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "raytracing2-fork_amd"))
+import torch  # noqa: E402,F401  (one HIP runtime)
+import rt2  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="B")
+ap.add_argument("--variants", default="1,3,0,4,5,6,2,7,8")
+ap.add_argument("--rounds", type=int, default=3)
+ap.add_argument("--width", type=int, default=0)
+ap.add_argument("--height", type=int, default=0)
+ap.add_argument("--rays", type=int, default=0)
+a = ap.parse_args()
+sd, spec = rt2.build_config_scene(a.config)
+W, H, R = a.width or spec.width, a.height or spec.height, a.rays or spec.rays
+u = rt2.offline_uniforms(W, H, spec.bounces, R, sd.num_triangles)
+scene = rt2.Scene(sd, 0)
+variants = [int(v) for v in a.variants.split(",")]
+times = {v: [] for v in variants}
+ref = None
+for rnd in range(a.rounds):
+    for v in variants:
+        scene.set_variant(v)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        img = scene.render_host(u, 0, spec.frames)
+        times[v].append(time.perf_counter() - t)
+        if rnd == 0:
+            if ref is None:
+                ref = img
+            assert np.array_equal(img, ref), f"variant {v} differs"
+st = scene.stats(reset=True)
+samples = W * H * R * spec.frames
+out = {}
+for v in variants:
+    med = float(np.median(times[v]))
+    out[rt2.lib().rt2_variant_name(v).decode()] = dict(variant=v, median_ms=round(med * 1e3, 2),
+                                                        min_ms=round(min(times[v]) * 1e3, 2),
+                                                        msamples_s=round(samples / med / 1e6, 2))
+print(json.dumps({"config": a.config, "W": W, "H": H, "R": R, "segments_per_sample":
+                  st.segments / (samples * a.rounds * len(variants)), "variants": out}, indent=1))
