@@ -144,6 +144,52 @@ __device__ __forceinline__ void mt_test_filtered(const f3& o, const f3& d, float
     }
 }
 
+// Filter part of mt_test_filtered only (branch-free): true when triangle
+// {t0,t1,t2} may update the closest hit.
+__device__ __forceinline__ bool mt_filter(const f3& o, const f3& d, float4 t0, float4 t1, float4 t2, float bestK) {
+    const f3 a = mk(t0.x, t0.y, t0.z);
+    const f3 e0 = mk(t0.w, t1.x, t1.y);
+    const f3 e1 = mk(t1.z, t1.w, t2.x);
+    const f3 n = mk(t2.y, t2.z, t2.w);
+    const float det = -dot(d, n);
+    const f3 ao = sub(o, a);
+    const float tnum = dot(ao, n);
+    const f3 q = cross(d, ao);
+    const float U = dot(e1, q);
+    const float V = dot(e0, q);
+    const float B = det * 0x1p-60f;
+    return (tnum > 0.0f) & (U <= B) & (V >= -B) & ((V - U) <= det * 1.0009765625f) & (tnum <= det * bestK);
+}
+
+// Two-phase sweep over [begin, end) of the LDS array (triangle indices base+k):
+// phase 1 evaluates the filter of G triangles branch-free (G independent
+// dependency chains, 3G LDS reads in flight), phase 2 runs the exact test
+// (mt_test_filtered) for the surviving bits in increasing index order — the
+// same update sequence as testing every triangle in order.
+template <int G>
+__device__ __forceinline__ void sweep_grouped(const f3& o, const f3& d, const float4* lds, int count, int base,
+                                              float& best, int& bi, float& bestK) {
+    int i = 0;
+    for (; i + G <= count; i += G) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int k = 0; k < G; k++) {
+            const float4* t = lds + 3 * (i + k);
+            m |= (uint32_t)mt_filter(o, d, t[0], t[1], t[2], bestK) << k;
+        }
+        while (m) {
+            const int k = __builtin_ctz(m);
+            m &= m - 1;
+            const float4* t = lds + 3 * (i + k);
+            mt_test_filtered(o, d, t[0], t[1], t[2], base + i + k, best, bi, bestK);
+        }
+    }
+    for (; i < count; i++) {
+        const float4* t = lds + 3 * i;
+        mt_test_filtered(o, d, t[0], t[1], t[2], base + i, best, bi, bestK);
+    }
+}
+
 template <int MT>
 __device__ __forceinline__ void mt_dispatch(const f3& o, const f3& d, float4 t0, float4 t1, float4 t2, int idx,
                                             float& best, int& best_i, float& bestK) {
@@ -372,9 +418,13 @@ __global__ __launch_bounds__(BLOCK) void render_resident(RenderParams p) {
             float best = 1e38f, bestK = 1e38f * 1.0009765625f;
             int bi = -1;
             const f3 o = L.o, d = L.d;
+            if constexpr (MT >= 2) {
+                sweep_grouped<MT>(o, d, lds, p.n_tris, 0, best, bi, bestK);
+            } else {
 #pragma unroll UNROLL
-            for (int i = 0; i < p.n_tris; i++) {
-                mt_dispatch<MT>(o, d, lds[3 * i], lds[3 * i + 1], lds[3 * i + 2], i, best, bi, bestK);
+                for (int i = 0; i < p.n_tris; i++) {
+                    mt_dispatch<MT>(o, d, lds[3 * i], lds[3 * i + 1], lds[3 * i + 2], i, best, bi, bestK);
+                }
             }
             shade(L, p, best, bi);
         }
@@ -407,9 +457,13 @@ __global__ __launch_bounds__(BLOCK) void render_tiled(RenderParams p) {
             for (int i = threadIdx.x; i < 3 * cnt; i += BLOCK) lds[i] = p.tri[3 * base + i];
             __syncthreads();
             if (tracing) {
+                if constexpr (MT >= 2) {
+                    sweep_grouped<MT>(o, d, lds, cnt, base, best, bi, bestK);
+                } else {
 #pragma unroll UNROLL
-                for (int i = 0; i < cnt; i++)
-                    mt_dispatch<MT>(o, d, lds[3 * i], lds[3 * i + 1], lds[3 * i + 2], base + i, best, bi, bestK);
+                    for (int i = 0; i < cnt; i++)
+                        mt_dispatch<MT>(o, d, lds[3 * i], lds[3 * i + 1], lds[3 * i + 2], base + i, best, bi, bestK);
+                }
             }
         }
         if (tracing) {
@@ -639,6 +693,12 @@ const Variant kVariants[] = {
     RT2_VARIANT(false, 512, 1, 8, "resident/512/filtered/u8"),   // 6
     RT2_VARIANT(true, 512, 1, 4, "tiled/512/filtered/u4"),       // 7
     RT2_VARIANT(true, 1024, 1, 4, "tiled/1024/filtered/u4"),     // 8
+    RT2_VARIANT(false, 512, 4, 1, "resident/512/grouped4"),      // 9
+    RT2_VARIANT(false, 512, 8, 1, "resident/512/grouped8"),      // 10
+    RT2_VARIANT(false, 1024, 4, 1, "resident/1024/grouped4"),    // 11
+    RT2_VARIANT(false, 256, 4, 1, "resident/256/grouped4"),      // 12
+    RT2_VARIANT(true, 512, 4, 1, "tiled/512/grouped4"),          // 13
+    RT2_VARIANT(false, 512, 2, 1, "resident/512/grouped2"),      // 14
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr size_t kResidentMaxBytes = 112 * 1024;

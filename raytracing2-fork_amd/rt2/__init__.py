@@ -254,8 +254,11 @@ class SceneData:
             raise RT2Error("rt2_sd_create failed")
 
     def __del__(self):
-        if getattr(self, "_p", None):
-            lib().rt2_sd_destroy(self._p)
+        if getattr(self, "_p", None) and _lib is not None:
+            try:
+                _lib.rt2_sd_destroy(self._p)
+            except Exception:  # interpreter shutdown
+                pass
             self._p = None
 
     def load_obj_folder(self, folder: str) -> None:  # getTrianglesData_, mesh.h:279-613
@@ -391,12 +394,15 @@ class Scene:
         self._p = p
 
     def close(self):
-        if getattr(self, "_p", None):
-            lib().rt2_scene_destroy(self._p)
+        if getattr(self, "_p", None) and _lib is not None:
+            _lib.rt2_scene_destroy(self._p)
             self._p = None
 
     def __del__(self):
-        self.close()
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown
+            pass
 
     def set_variant(self, v: int) -> int:
         return lib().rt2_scene_set_variant(self._p, v)
