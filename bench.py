@@ -195,7 +195,7 @@ def main():
                    "tile_rows": args.tile_rows},
         "roofline": {"bound": "valu", "achieved": round(flops, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(flops / VALU_PEAK_TFLOPS, 4), "traffic": None,
-                     "kernel": "render_resident (rt2_render.hip)", "kernel_ms": round(kern_ms, 3),
+                     "kernel": "render_smem (rt2_render.hip, variant smem/256/masked8/coop32)", "kernel_ms": round(kern_ms, 3),
                      "tests_per_launch": int(tests_per_launch),
                      "segments_per_sample": round(segs / (samples_per_step * args.steps), 4),
                      "hbm_read_algorithmic": {"achieved": round(hbm_read, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -166,9 +166,17 @@ __device__ __forceinline__ bool mt_filter(const f3& o, const f3& d, float4 t0, f
 // dependency chains, 3G LDS reads in flight), phase 2 runs the exact test
 // (mt_test_filtered) for the surviving bits in increasing index order — the
 // same update sequence as testing every triangle in order.
-template <int G>
+// Diagnostic counters of the grouped sweep (STATS variants only).
+struct SweepStats {
+    uint32_t groups = 0;         // phase-1 groups evaluated (per wave)
+    uint32_t groups_exact = 0;   // groups where some lane had a survivor (per wave)
+    uint32_t exact_iters = 0;    // phase-2 iterations executed by the wave
+    uint32_t lane_survivors = 0; // survivor bits summed over lanes
+};
+
+template <int G, bool STATS = false>
 __device__ __forceinline__ void sweep_grouped(const f3& o, const f3& d, const float4* lds, int count, int base,
-                                              float& best, int& bi, float& bestK) {
+                                              float& best, int& bi, float& bestK, SweepStats* ss = nullptr) {
     int i = 0;
     for (; i + G <= count; i += G) {
         uint32_t m = 0;
@@ -176,6 +184,16 @@ __device__ __forceinline__ void sweep_grouped(const f3& o, const f3& d, const fl
         for (int k = 0; k < G; k++) {
             const float4* t = lds + 3 * (i + k);
             m |= (uint32_t)mt_filter(o, d, t[0], t[1], t[2], bestK) << k;
+        }
+        if constexpr (STATS) {
+            ss->groups += 1;
+            ss->lane_survivors += __popc(m);
+            if (__any(m != 0)) ss->groups_exact += 1;
+            uint32_t mm = m;
+            while (__any(mm != 0)) {
+                ss->exact_iters += 1;
+                mm &= mm - 1;
+            }
         }
         while (m) {
             const int k = __builtin_ctz(m);
@@ -190,6 +208,205 @@ __device__ __forceinline__ void sweep_grouped(const f3& o, const f3& d, const fl
     }
 }
 
+// Scalar-path sweep: the triangle records are wave-uniform, so they are read
+// with scalar loads (constant address space -> s_load_dwordx4 into SGPRs,
+// through the scalar cache) and fed to the VALU as SGPR operands; no LDS, no
+// VGPRs for triangle data.  Same two-phase structure as sweep_grouped.
+typedef const __attribute__((address_space(4))) float cfloat;
+__device__ __forceinline__ float4 ldc4(cfloat* p) { return make_float4(p[0], p[1], p[2], p[3]); }
+template <int G>
+__device__ __forceinline__ void sweep_smem(const f3& o, const f3& d, cfloat* tri, int count, float& best, int& bi,
+                                           float& bestK) {
+    int i = 0;
+    for (; i + G <= count; i += G) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int k = 0; k < G; k++) {
+            cfloat* t = tri + 12 * (i + k);
+            m |= (uint32_t)mt_filter(o, d, ldc4(t), ldc4(t + 4), ldc4(t + 8), bestK) << k;
+        }
+        while (m) {
+            const int k = __builtin_ctz(m);
+            m &= m - 1;
+            cfloat* t = tri + 12 * (i + k);
+            mt_test_filtered(o, d, ldc4(t), ldc4(t + 4), ldc4(t + 8), i + k, best, bi, bestK);
+        }
+    }
+    for (; i < count; i++) {
+        cfloat* t = tri + 12 * i;
+        mt_test_filtered(o, d, ldc4(t), ldc4(t + 4), ldc4(t + 8), i, best, bi, bestK);
+    }
+}
+
+// Exact intermediates of one test (phase 1 output, reused by phase 2).
+struct MtQ {
+    float det, tnum, U, V;
+};
+__device__ __forceinline__ MtQ mt_quantities(const f3& o, const f3& d, float4 t0, float4 t1, float4 t2) {
+    const f3 a = mk(t0.x, t0.y, t0.z);
+    const f3 e0 = mk(t0.w, t1.x, t1.y);
+    const f3 e1 = mk(t1.z, t1.w, t2.x);
+    const f3 n = mk(t2.y, t2.z, t2.w);
+    MtQ r;
+    r.det = -dot(d, n);
+    const f3 ao = sub(o, a);
+    r.tnum = dot(ao, n);
+    const f3 q = cross(d, ao);
+    r.U = dot(e1, q);
+    r.V = dot(e0, q);
+    return r;
+}
+__device__ __forceinline__ bool mt_pass(const MtQ& q, float bestK) {
+    const float B = q.det * 0x1p-60f;
+    return (q.tnum > 0.0f) & (q.U <= B) & (q.V >= -B) & ((q.V - q.U) <= q.det * 1.0009765625f) &
+           (q.tnum <= q.det * bestK);
+}
+// compute.glsl:312-327 on the phase-1 intermediates (exactly the reference arithmetic).
+__device__ __forceinline__ void mt_exact(const MtQ& q, int idx, float& best, int& bi, float& bestK) {
+    if (!((q.det < 1e-10f && q.det > -1e-10f) || q.det < 0.0f)) {
+        const float inv = 1.0f / q.det;
+        const float dst = q.tnum * inv;
+        const float u = -q.U * inv;
+        const float v = q.V * inv;
+        if (!(dst <= 1e-6f) && !(u < 0.0f || v < 0.0f || 1.0f - u - v < 0.0f) && dst < best) {
+            best = dst;
+            bi = idx;
+            bestK = best * 1.0009765625f;
+        }
+    }
+}
+
+// Masked two-phase sweep: phase 1 computes the intermediates and the filter of
+// G triangles (the G predicates stay wave lane-masks in SGPR pairs, no
+// per-lane bit packing); phase 2 runs mt_exact under each mask in index order
+// (skipped by a scalar branch when the mask is empty).  SMEM selects the
+// scalar-load path for the triangle records instead of LDS.
+template <int G, bool SMEM>
+__device__ __forceinline__ void sweep_masked(const f3& o, const f3& d, const float4* lds, const float* gtri,
+                                             int count, int base, float& best, int& bi, float& bestK) {
+    int i = 0;
+    for (; i + G <= count; i += G) {
+        MtQ q[G];
+        bool f[G];
+#pragma unroll
+        for (int k = 0; k < G; k++) {
+            float4 t0, t1, t2;
+            if constexpr (SMEM) {
+                cfloat* t = (cfloat*)gtri + 12 * (i + k);
+                t0 = ldc4(t);
+                t1 = ldc4(t + 4);
+                t2 = ldc4(t + 8);
+            } else {
+                const float4* t = lds + 3 * (i + k);
+                t0 = t[0];
+                t1 = t[1];
+                t2 = t[2];
+            }
+            q[k] = mt_quantities(o, d, t0, t1, t2);
+            f[k] = mt_pass(q[k], bestK);
+        }
+#pragma unroll
+        for (int k = 0; k < G; k++)
+            if (f[k]) mt_exact(q[k], base + i + k, best, bi, bestK);
+    }
+    for (; i < count; i++) {
+        float4 t0, t1, t2;
+        if constexpr (SMEM) {
+            cfloat* t = (cfloat*)gtri + 12 * i;
+            t0 = ldc4(t);
+            t1 = ldc4(t + 4);
+            t2 = ldc4(t + 8);
+        } else {
+            const float4* t = lds + 3 * i;
+            t0 = t[0];
+            t1 = t[1];
+            t2 = t[2];
+        }
+        const MtQ q = mt_quantities(o, d, t0, t1, t2);
+        if (mt_pass(q, bestK)) mt_exact(q, base + i, best, bi, bestK);
+    }
+}
+
+// Lean masked sweep: like sweep_masked, but phase 1 keeps ONLY the G filter
+// lane-masks (SGPRs) live; phase 2 (entered for ~5% of groups on config B)
+// reloads the surviving triangle and recomputes its intermediates.  Frees the
+// 4*G VGPRs sweep_masked holds across the group.
+__device__ __forceinline__ void load_tri(const float4* lds, const float* gtri, bool smem, int i, float4& t0,
+                                         float4& t1, float4& t2) {
+    if (smem) {
+        cfloat* t = (cfloat*)gtri + 12 * i;
+        t0 = ldc4(t);
+        t1 = ldc4(t + 4);
+        t2 = ldc4(t + 8);
+    } else {
+        const float4* t = lds + 3 * i;
+        t0 = t[0];
+        t1 = t[1];
+        t2 = t[2];
+    }
+}
+template <int G, bool SMEM>
+__device__ __forceinline__ void sweep_lean(const f3& o, const f3& d, const float4* lds, const float* gtri, int count,
+                                           int base, float& best, int& bi, float& bestK) {
+    int i = 0;
+    for (; i + G <= count; i += G) {
+        bool f[G];
+#pragma unroll
+        for (int k = 0; k < G; k++) {
+            float4 t0, t1, t2;
+            load_tri(lds, gtri, SMEM, i + k, t0, t1, t2);
+            f[k] = mt_pass(mt_quantities(o, d, t0, t1, t2), bestK);
+        }
+#pragma unroll
+        for (int k = 0; k < G; k++) {
+            if (f[k]) {
+                // opaque index: force a reload + recompute instead of keeping
+                // phase 1's intermediates live across the group
+                int j = i + k;
+                asm volatile("" : "+s"(j));
+                float4 t0, t1, t2;
+                load_tri(lds, gtri, SMEM, j, t0, t1, t2);
+                mt_exact(mt_quantities(o, d, t0, t1, t2), base + j, best, bi, bestK);
+            }
+        }
+    }
+    for (; i < count; i++) {
+        float4 t0, t1, t2;
+        load_tri(lds, gtri, SMEM, i, t0, t1, t2);
+        const MtQ q = mt_quantities(o, d, t0, t1, t2);
+        if (mt_pass(q, bestK)) mt_exact(q, base + i, best, bi, bestK);
+    }
+}
+
+// Cooperative closest hit for the drain phase: all 64 lanes sweep ONE ray
+// (lane l tests triangles l, l+64, ... in increasing order with its own
+// running best) and the wave reduces (dst, index) lexicographically.  The
+// result equals the sequential strict-< scan: the minimum distance, and among
+// exact ties the lowest index.  Triangle records are read from `tris`
+// (LDS or global) with per-lane addresses.
+__device__ __forceinline__ void coop_closest(const f3& o, const f3& d, const float4* tris, int n, float& best_out,
+                                             int& bi_out) {
+    const int lane = (int)lane_id();
+    float best = 1e38f, bestK = 1e38f * 1.0009765625f;
+    int bi = -1;
+    for (int i = lane; i < n; i += 64) {
+        const float4* t = tris + 3 * i;
+        const MtQ q = mt_quantities(o, d, t[0], t[1], t[2]);
+        if (mt_pass(q, bestK)) mt_exact(q, i, best, bi, bestK);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const float ob = __shfl_xor(best, off);
+        const int oi = __shfl_xor(bi, off);
+        const bool take = (ob < best) || (ob == best && oi >= 0 && (bi < 0 || oi < bi));
+        if (take) {
+            best = ob;
+            bi = oi;
+        }
+    }
+    best_out = best;
+    bi_out = bi;
+}
+
 template <int MT>
 __device__ __forceinline__ void mt_dispatch(const f3& o, const f3& d, float4 t0, float4 t1, float4 t2, int idx,
                                             float& best, int& best_i, float& bestK) {
@@ -199,18 +416,19 @@ __device__ __forceinline__ void mt_dispatch(const f3& o, const f3& d, float4 t0,
         mt_test_filtered(o, d, t0, t1, t2, idx, best, best_i, bestK);
 }
 
+// Per-lane path state, kept small (VGPRs decide the waves per SIMD): the
+// camera end point is recomputed per ray and the frame sums go straight to the
+// accumulators in HBM (one read-modify-write per pixel-frame).
 struct Lane {
     int st;
-    unsigned long long item;
+    uint32_t item;
     int x, y;
     uint32_t frame;  // frames done for this item
     uint32_t seed;
     int ray;
     int bounce;
     bool inside;
-    f3 o, d, rayColor, incoming, colorCum, endPoint;
-    f3 acc;
-    uint32_t a8x, a8y, a8z;
+    f3 o, d, rayColor, incoming, colorCum;
     uint32_t segs;
 };
 
@@ -228,19 +446,11 @@ __device__ __forceinline__ void advance(Lane& L, const RenderParams& p) {
             if (need) {
                 unsigned long long it = base + lanes_below(m);
                 if (it < p.n_items) {
-                    L.item = it;
-                    int lr = (int)(it / (unsigned long long)p.W);
-                    L.x = (int)(it - (unsigned long long)lr * (unsigned long long)p.W);
+                    L.item = (uint32_t)it;
+                    int lr = (int)(L.item / (uint32_t)p.W);
+                    L.x = (int)(L.item - (uint32_t)lr * (uint32_t)p.W);
                     L.y = shard_row(lr, p.tile_rows, p.rank, p.nranks);
                     L.frame = 0;
-                    float4 a = p.accum[it];
-                    L.acc = mk(a.x, a.y, a.z);
-                    if (p.accum8) {
-                        uint4 q = p.accum8[it];
-                        L.a8x = q.x;
-                        L.a8y = q.y;
-                        L.a8z = q.z;
-                    }
                     L.st = ST_NEW_FRAME;
                 } else {
                     L.st = ST_DONE;
@@ -250,22 +460,23 @@ __device__ __forceinline__ void advance(Lane& L, const RenderParams& p) {
         if (L.st == ST_NEW_FRAME) {
             // compute.glsl:662-670
             const uint32_t f = p.frame_begin + L.frame;
-            float px = (float)(L.x * 2 - p.W) / (float)p.W;
-            float py = (float)(L.y * 2 - p.H) / (float)p.H;
             L.seed = (uint32_t)L.x + (uint32_t)L.y * (uint32_t)p.W + f * 968824447u;
-            L.endPoint = add(add(add(ld3(p.cam), ld3(p.vpFront)), muls(ld3(p.vpRight), px)), muls(ld3(p.vpUp), py));
             L.colorCum = mk(0.0f, 0.0f, 0.0f);
             L.ray = 0;
             L.st = ST_NEW_RAY;
         }
         if (L.st == ST_NEW_RAY) {
-            // compute.glsl:685-690
+            // compute.glsl:665-670 (endPoint, recomputed per ray) and :685-690
+            const float px = (float)(L.x * 2 - p.W) / (float)p.W;
+            const float py = (float)(L.y * 2 - p.H) / (float)p.H;
+            const f3 endPoint =
+                add(add(add(ld3(p.cam), ld3(p.vpFront)), muls(ld3(p.vpRight), px)), muls(ld3(p.vpUp), py));
             float ang = rnd(L.seed);
             float cs = rt2pm_cosf(ang), sn = rt2pm_sinf(ang);
             L.o = add(add(ld3(p.cam), muls(ld3(p.defR), cs)), muls(ld3(p.defU), sn));
             float jr = -0.5f + (0.5f - -0.5f) * rnd(L.seed);
             float ju = -0.5f + (0.5f - -0.5f) * rnd(L.seed);
-            f3 endJ = add(add(L.endPoint, muls(ld3(p.pixR), jr)), muls(ld3(p.pixU), ju));
+            f3 endJ = add(add(endPoint, muls(ld3(p.pixR), jr)), muls(ld3(p.pixU), ju));
             L.d = normalize(sub(endJ, L.o));
             L.inside = false;
             L.rayColor = mk(1.0f, 1.0f, 1.0f);
@@ -289,19 +500,18 @@ __device__ __forceinline__ void end_path(Lane& L, const RenderParams& p) {
     }
     f3 c = divs(L.colorCum, (float)p.R);
     c = mk(srgb1(aces1(c.x)), srgb1(aces1(c.y)), srgb1(aces1(c.z)));
-    L.acc = add(L.acc, c);
-    // GL float -> unorm8, round to nearest (GL 4.3 §2.3.5.2)
-    L.a8x += (uint32_t)(clampf(c.x, 0.0f, 1.0f) * 255.0f + 0.5f);
-    L.a8y += (uint32_t)(clampf(c.y, 0.0f, 1.0f) * 255.0f + 0.5f);
-    L.a8z += (uint32_t)(clampf(c.z, 0.0f, 1.0f) * 255.0f + 0.5f);
-    L.frame += 1;
-    if (L.frame < p.frame_count) {
-        L.st = ST_NEW_FRAME;
-        return;
+    // accumulate this frame in frame order: acc = acc + colour
+    const float4 a = p.accum[L.item];
+    p.accum[L.item] = make_float4(a.x + c.x, a.y + c.y, a.z + c.z, 0.0f);
+    if (p.accum8) {
+        // GL float -> unorm8, round to nearest (GL 4.3 §2.3.5.2)
+        const uint4 q = p.accum8[L.item];
+        p.accum8[L.item] = make_uint4(q.x + (uint32_t)(clampf(c.x, 0.0f, 1.0f) * 255.0f + 0.5f),
+                                      q.y + (uint32_t)(clampf(c.y, 0.0f, 1.0f) * 255.0f + 0.5f),
+                                      q.z + (uint32_t)(clampf(c.z, 0.0f, 1.0f) * 255.0f + 0.5f), 0u);
     }
-    p.accum[L.item] = make_float4(L.acc.x, L.acc.y, L.acc.z, 0.0f);
-    if (p.accum8) p.accum8[L.item] = make_uint4(L.a8x, L.a8y, L.a8z, 0u);
-    L.st = ST_NEED_ITEM;
+    L.frame += 1;
+    L.st = L.frame < p.frame_count ? ST_NEW_FRAME : ST_NEED_ITEM;
 }
 
 // Phase C: scatter at the closest hit (compute.glsl:485-559).
@@ -388,8 +598,7 @@ __device__ __forceinline__ void lane_init(Lane& L) {
     L.ray = 0;
     L.bounce = 0;
     L.inside = false;
-    L.o = L.d = L.rayColor = L.incoming = L.colorCum = L.endPoint = L.acc = mk(0.0f, 0.0f, 0.0f);
-    L.a8x = L.a8y = L.a8z = 0;
+    L.o = L.d = L.rayColor = L.incoming = L.colorCum = mk(0.0f, 0.0f, 0.0f);
     L.segs = 0;
 }
 
@@ -402,6 +611,9 @@ __device__ __forceinline__ void flush_counters(const Lane& L, const RenderParams
 // RESIDENT: all triangles in LDS, waves independent after the initial load.
 template <int BLOCK, int MT, int UNROLL>
 __global__ __launch_bounds__(BLOCK) void render_resident(RenderParams p) {
+    // UNROLL == 0 on a grouped variant = diagnostic build with sweep counters
+    constexpr bool kStats = MT >= 2 && UNROLL == 0;
+    SweepStats ss;
     extern __shared__ float4 lds[];
     const int n4 = 3 * p.n_tris;
     for (int i = threadIdx.x; i < n4; i += BLOCK) lds[i] = p.tri[i];
@@ -418,8 +630,12 @@ __global__ __launch_bounds__(BLOCK) void render_resident(RenderParams p) {
             float best = 1e38f, bestK = 1e38f * 1.0009765625f;
             int bi = -1;
             const f3 o = L.o, d = L.d;
-            if constexpr (MT >= 2) {
-                sweep_grouped<MT>(o, d, lds, p.n_tris, 0, best, bi, bestK);
+            if constexpr (MT >= 200) {
+                sweep_lean<MT - 200, false>(o, d, lds, nullptr, p.n_tris, 0, best, bi, bestK);
+            } else if constexpr (MT >= 100) {
+                sweep_masked<MT - 100, false>(o, d, lds, nullptr, p.n_tris, 0, best, bi, bestK);
+            } else if constexpr (MT >= 2) {
+                sweep_grouped<MT, kStats>(o, d, lds, p.n_tris, 0, best, bi, bestK, &ss);
             } else {
 #pragma unroll UNROLL
                 for (int i = 0; i < p.n_tris; i++) {
@@ -430,6 +646,20 @@ __global__ __launch_bounds__(BLOCK) void render_resident(RenderParams p) {
         }
     }
     flush_counters(L, p);
+    if constexpr (kStats) {
+        unsigned long long surv = ss.lane_survivors;
+        for (int off = 32; off > 0; off >>= 1) surv += __shfl_xor(surv, off);
+        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+        if (lane_id() == 0) {
+            atomicAdd(p.seg_counter + 1, (unsigned long long)ss.groups);
+            atomicAdd(p.seg_counter + 2, (unsigned long long)ss.groups_exact);
+            atomicAdd(p.seg_counter + 3, (unsigned long long)ss.exact_iters);
+            atomicAdd(p.seg_counter + 4, surv);
+            // wave finish-time spread: [6] = earliest wave end, [5] = latest (ticks of 10 ns)
+            atomicMin(p.seg_counter + 5, t_end);
+            atomicMax(p.seg_counter + 4 + 2, t_end);
+        }
+    }
 }
 
 // TILED: triangles streamed through LDS; the workgroup sweeps in lockstep.
@@ -457,7 +687,9 @@ __global__ __launch_bounds__(BLOCK) void render_tiled(RenderParams p) {
             for (int i = threadIdx.x; i < 3 * cnt; i += BLOCK) lds[i] = p.tri[3 * base + i];
             __syncthreads();
             if (tracing) {
-                if constexpr (MT >= 2) {
+                if constexpr (MT >= 100) {
+                    sweep_masked<MT - 100, false>(o, d, lds, nullptr, cnt, base, best, bi, bestK);
+                } else if constexpr (MT >= 2) {
                     sweep_grouped<MT>(o, d, lds, cnt, base, best, bi, bestK);
                 } else {
 #pragma unroll UNROLL
@@ -469,6 +701,62 @@ __global__ __launch_bounds__(BLOCK) void render_tiled(RenderParams p) {
         if (tracing) {
             L.bounce += 1;
             L.segs += 1;
+            shade(L, p, best, bi);
+        }
+    }
+    flush_counters(L, p);
+}
+
+// SMEM: no LDS; triangles reach the VALU through the scalar cache (sweep_smem).
+// COOP > 0: drain mode — once the item pool is exhausted (some lane is DONE)
+// and at most COOP lanes of the wave still trace, each live ray's closest hit
+// is computed by the whole wave (coop_closest), one ray at a time.
+template <int BLOCK, int G, int COOP>
+__global__ __launch_bounds__(BLOCK) void render_smem(RenderParams p) {
+    cfloat* tri = (cfloat*)p.tri;
+    Lane L;
+    lane_init(L);
+    for (;;) {
+        advance(L, p);
+        const unsigned long long act = __ballot(L.st == ST_TRACE);
+        if (!act) break;
+        if (COOP > 0 && __popcll(act) <= (unsigned)COOP && __any(L.st == ST_DONE)) {
+            float mybest = 1e38f;
+            int mybi = -1;
+            unsigned long long m = act;
+            while (m) {
+                const int j = __builtin_ctzll(m);
+                m &= m - 1;
+                const f3 oj = mk(__shfl(L.o.x, j), __shfl(L.o.y, j), __shfl(L.o.z, j));
+                const f3 dj = mk(__shfl(L.d.x, j), __shfl(L.d.y, j), __shfl(L.d.z, j));
+                float b;
+                int bidx;
+                coop_closest(oj, dj, p.tri, p.n_tris, b, bidx);
+                if ((int)lane_id() == j) {
+                    mybest = b;
+                    mybi = bidx;
+                }
+            }
+            if (L.st == ST_TRACE) {
+                L.bounce += 1;
+                L.segs += 1;
+                shade(L, p, mybest, mybi);
+            }
+            continue;
+        }
+        if (L.st == ST_TRACE) {
+            L.bounce += 1;
+            L.segs += 1;
+            float best = 1e38f, bestK = 1e38f * 1.0009765625f;
+            int bi = -1;
+            const f3 o = L.o, d = L.d;
+            if constexpr (G >= 200)
+                sweep_lean<G - 200, true>(o, d, nullptr, (const float*)p.tri, p.n_tris, 0, best, bi, bestK);
+            else if constexpr (G >= 100)
+                sweep_masked<G - 100, true>(o, d, nullptr, p.tri ? (const float*)p.tri : nullptr, p.n_tris, 0, best,
+                                            bi, bestK);
+            else
+                sweep_smem<G>(o, d, tri, p.n_tris, best, bi, bestK);
             shade(L, p, best, bi);
         }
     }
@@ -567,6 +855,7 @@ struct rt2_scene {
     unsigned long long samples = 0, tests_per_seg = 0;
     int variant = 0;
     int last_variant = -1;
+    unsigned long long diag[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int num_cus = 256;
     size_t max_lds = 65536;
 };
@@ -605,8 +894,8 @@ extern "C" int rt2_scene_create(const rt2_triangle* tris, int32_t n_tris, const 
     HIPCHECK(hipMalloc(&s->d_tri, nt * 3 * sizeof(float4)));
     HIPCHECK(hipMalloc(&s->d_mtl, nt * sizeof(int)));
     HIPCHECK(hipMalloc(&s->d_mats, (size_t)n_mats * sizeof(rt2_material)));
-    HIPCHECK(hipMalloc(&s->d_counters, 4 * sizeof(unsigned long long)));
-    HIPCHECK(hipMemset(s->d_counters, 0, 4 * sizeof(unsigned long long)));
+    HIPCHECK(hipMalloc(&s->d_counters, 8 * sizeof(unsigned long long)));
+    HIPCHECK(hipMemset(s->d_counters, 0, 8 * sizeof(unsigned long long)));
     if (n_tris > 0) HIPCHECK(hipMemcpy(s->d_raw, tris, (size_t)n_tris * sizeof(rt2_triangle), hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(s->d_mats, mats, (size_t)n_mats * sizeof(rt2_material), hipMemcpyHostToDevice));
     if (s->n_nodes > 0) {
@@ -658,50 +947,78 @@ namespace {
 constexpr int kTileTris = 1024;  // 48 KiB of LDS per tile
 
 // Kernel variants (rt2_scene_set_variant); 0 = auto = the default below.
+enum Kind : int { K_RESIDENT = 0, K_TILED = 1, K_SMEM = 2 };
 struct Variant {
-    bool tiled;
+    int kind;
     int block;
     hipError_t (*launch)(const RenderParams&, int blocks, size_t lds, hipStream_t st);
     hipError_t (*occupancy)(int* occ, size_t lds);
     const char* name;
 };
 
-template <bool TILED, int BLOCK, int MT, int UNROLL>
+template <int KIND, int BLOCK, int MT, int UNROLL>
 hipError_t launch_t(const RenderParams& p, int blocks, size_t lds, hipStream_t st) {
-    if constexpr (TILED)
+    if constexpr (KIND == K_TILED)
         hipLaunchKernelGGL((render_tiled<BLOCK, MT, UNROLL>), dim3(blocks), dim3(BLOCK), lds, st, p);
+    else if constexpr (KIND == K_SMEM)
+        hipLaunchKernelGGL((render_smem<BLOCK, MT % 1000, MT / 1000>), dim3(blocks), dim3(BLOCK), 0, st, p);
     else
         hipLaunchKernelGGL((render_resident<BLOCK, MT, UNROLL>), dim3(blocks), dim3(BLOCK), lds, st, p);
     return hipGetLastError();
 }
-template <bool TILED, int BLOCK, int MT, int UNROLL>
+template <int KIND, int BLOCK, int MT, int UNROLL>
 hipError_t occ_t(int* occ, size_t lds) {
-    if constexpr (TILED)
+    if constexpr (KIND == K_TILED)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_tiled<BLOCK, MT, UNROLL>, BLOCK, lds);
+    else if constexpr (KIND == K_SMEM)
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_smem<BLOCK, MT % 1000, MT / 1000>, BLOCK, 0);
     else
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_resident<BLOCK, MT, UNROLL>, BLOCK, lds);
 }
 #define RT2_VARIANT(T, B, M, U, NAME) Variant{T, B, launch_t<T, B, M, U>, occ_t<T, B, M, U>, NAME}
 
 const Variant kVariants[] = {
-    RT2_VARIANT(false, 512, 1, 4, "resident/512/filtered/u4"),   // 0: default (resident)
-    RT2_VARIANT(false, 256, 0, 4, "resident/256/plain/u4"),      // 1: round-1 v1 kernel
-    RT2_VARIANT(true, 256, 1, 4, "tiled/256/filtered/u4"),       // 2: default (tiled)
-    RT2_VARIANT(false, 256, 1, 4, "resident/256/filtered/u4"),   // 3
-    RT2_VARIANT(false, 1024, 1, 4, "resident/1024/filtered/u4"), // 4
-    RT2_VARIANT(false, 512, 1, 2, "resident/512/filtered/u2"),   // 5
-    RT2_VARIANT(false, 512, 1, 8, "resident/512/filtered/u8"),   // 6
-    RT2_VARIANT(true, 512, 1, 4, "tiled/512/filtered/u4"),       // 7
-    RT2_VARIANT(true, 1024, 1, 4, "tiled/1024/filtered/u4"),     // 8
-    RT2_VARIANT(false, 512, 4, 1, "resident/512/grouped4"),      // 9
-    RT2_VARIANT(false, 512, 8, 1, "resident/512/grouped8"),      // 10
-    RT2_VARIANT(false, 1024, 4, 1, "resident/1024/grouped4"),    // 11
-    RT2_VARIANT(false, 256, 4, 1, "resident/256/grouped4"),      // 12
-    RT2_VARIANT(true, 512, 4, 1, "tiled/512/grouped4"),          // 13
-    RT2_VARIANT(false, 512, 2, 1, "resident/512/grouped2"),      // 14
+    RT2_VARIANT(K_SMEM, 256, 32108, 1, "smem/256/masked8/coop32"),   // 0: default (<= kSmemMaxTris)
+    RT2_VARIANT(K_RESIDENT, 256, 0, 4, "resident/256/plain/u4"),     // 1: round-1 v1 kernel
+    RT2_VARIANT(K_TILED, 512, 4, 1, "tiled/512/grouped4"),           // 2: default (large scenes)
+    RT2_VARIANT(K_RESIDENT, 256, 1, 4, "resident/256/filtered/u4"),  // 3
+    RT2_VARIANT(K_RESIDENT, 1024, 1, 4, "resident/1024/filtered/u4"),// 4
+    RT2_VARIANT(K_RESIDENT, 512, 1, 4, "resident/512/filtered/u4"),  // 5
+    RT2_VARIANT(K_RESIDENT, 512, 1, 8, "resident/512/filtered/u8"),  // 6
+    RT2_VARIANT(K_TILED, 256, 1, 4, "tiled/256/filtered/u4"),        // 7
+    RT2_VARIANT(K_TILED, 1024, 4, 1, "tiled/1024/grouped4"),         // 8
+    RT2_VARIANT(K_RESIDENT, 512, 4, 1, "resident/512/grouped4"),     // 9
+    RT2_VARIANT(K_RESIDENT, 1024, 8, 1, "resident/1024/grouped8"),   // 10
+    RT2_VARIANT(K_RESIDENT, 1024, 4, 1, "resident/1024/grouped4"),   // 11
+    RT2_VARIANT(K_RESIDENT, 256, 4, 1, "resident/256/grouped4"),     // 12
+    RT2_VARIANT(K_TILED, 512, 8, 1, "tiled/512/grouped8"),           // 13
+    RT2_VARIANT(K_RESIDENT, 512, 2, 1, "resident/512/grouped2"),     // 14
+    RT2_VARIANT(K_RESIDENT, 512, 4, 0, "resident/512/grouped4/STATS"), // 15: diagnostic counters
+    RT2_VARIANT(K_SMEM, 256, 4, 1, "smem/256/grouped4"),             // 16
+    RT2_VARIANT(K_SMEM, 512, 4, 1, "smem/512/grouped4"),             // 17
+    RT2_VARIANT(K_SMEM, 1024, 4, 1, "smem/1024/grouped4"),           // 18
+    RT2_VARIANT(K_SMEM, 512, 2, 1, "smem/512/grouped2"),             // 19
+    RT2_VARIANT(K_SMEM, 512, 8, 1, "smem/512/grouped8"),             // 20
+    RT2_VARIANT(K_RESIDENT, 512, 104, 1, "resident/512/masked4"),    // 21
+    RT2_VARIANT(K_RESIDENT, 512, 108, 1, "resident/512/masked8"),    // 22
+    RT2_VARIANT(K_SMEM, 256, 104, 1, "smem/256/masked4"),            // 23
+    RT2_VARIANT(K_SMEM, 256, 108, 1, "smem/256/masked8"),            // 24
+    RT2_VARIANT(K_SMEM, 512, 104, 1, "smem/512/masked4"),            // 25
+    RT2_VARIANT(K_TILED, 512, 104, 1, "tiled/512/masked4"),          // 26
+    RT2_VARIANT(K_SMEM, 256, 16108, 1, "smem/256/masked8/coop16"),   // 27
+    RT2_VARIANT(K_SMEM, 256, 32108, 1, "smem/256/masked8/coop32"),   // 28
+    RT2_VARIANT(K_SMEM, 256, 48108, 1, "smem/256/masked8/coop48"),   // 29
+    RT2_VARIANT(K_SMEM, 256, 64108, 1, "smem/256/masked8/coop64"),   // 30
+    RT2_VARIANT(K_SMEM, 256, 208, 1, "smem/256/lean8"),              // 31
+    RT2_VARIANT(K_SMEM, 256, 204, 1, "smem/256/lean4"),              // 32
+    RT2_VARIANT(K_RESIDENT, 1024, 208, 1, "resident/1024/lean8"),    // 33
+    RT2_VARIANT(K_RESIDENT, 1024, 204, 1, "resident/1024/lean4"),    // 34
+    RT2_VARIANT(K_RESIDENT, 512, 208, 1, "resident/512/lean8"),      // 35
+    RT2_VARIANT(K_SMEM, 512, 208, 1, "smem/512/lean8"),              // 36
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr size_t kResidentMaxBytes = 112 * 1024;
+constexpr int kSmemMaxTris = 16384;
 }  // namespace
 
 extern "C" const char* rt2_variant_name(int v) { return v >= 0 && v < kNumVariants ? kVariants[v].name : nullptr; }
@@ -760,6 +1077,10 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     p.rank = sh.rank;
     p.nranks = sh.nranks;
     p.n_items = (unsigned long long)rows * (unsigned long long)p.W;
+    if (p.n_items >= 0xffffffffull) {
+        rt2h::set_error("rt2_render: more than 2^32-1 pixels in one shard");
+        return -1;
+    }
     p.accum = reinterpret_cast<float4*>(d_accum);
     p.accum8 = reinterpret_cast<uint4*>(d_accum8);
     p.item_counter = s->d_counters;
@@ -767,13 +1088,18 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     p.tile_tris = kTileTris;
 
     HIPCHECK(hipMemsetAsync(s->d_counters, 0, sizeof(unsigned long long), st));
+    HIPCHECK(hipMemsetAsync(s->d_counters + 6, 0xff, sizeof(unsigned long long), st));  // diag: min wave end
+    HIPCHECK(hipMemsetAsync(s->d_counters + 7, 0, sizeof(unsigned long long), st));     // diag: max wave end
     const size_t resident_bytes = (size_t)3 * sizeof(float4) * (size_t)std::max(s->n_tris, 1);
     const bool fits = resident_bytes <= kResidentMaxBytes;
     int vi = s->variant;
-    if (vi <= 0 || vi >= kNumVariants) vi = fits ? 0 : 2;
-    if (!kVariants[vi].tiled && !fits) vi = 2;  // a resident variant cannot hold this scene
+    // auto: scalar-path kernel for small scenes (config B: 1,208 triangles),
+    // LDS-tiled sweep for large ones (config C/E: 100k-1M triangles)
+    if (vi <= 0 || vi >= kNumVariants) vi = s->n_tris <= kSmemMaxTris ? 0 : 2;
+    if (kVariants[vi].kind == K_RESIDENT && !fits) vi = 2;  // a resident variant cannot hold this scene
     const Variant& V = kVariants[vi];
-    const size_t lds = V.tiled ? (size_t)3 * sizeof(float4) * kTileTris : resident_bytes;
+    const size_t lds = V.kind == K_TILED ? (size_t)3 * sizeof(float4) * kTileTris
+                                         : (V.kind == K_SMEM ? 0 : resident_bytes);
     int occ = 0;
     HIPCHECK(V.occupancy(&occ, lds));
     occ = std::max(occ, 1);
@@ -795,8 +1121,9 @@ extern "C" int rt2_scene_stats(rt2_scene* s, rt2_stats* out, int reset) {
     }
     HIPCHECK(hipSetDevice(s->device));
     HIPCHECK(hipDeviceSynchronize());
-    unsigned long long c[4];
+    unsigned long long c[8];
     HIPCHECK(hipMemcpy(c, s->d_counters, sizeof(c), hipMemcpyDeviceToHost));
+    std::memcpy(s->diag, c, sizeof(c));
     out->samples = s->samples;
     out->segments = c[1];
     out->tests = c[1] * (unsigned long long)s->n_tris;
@@ -887,6 +1214,16 @@ extern "C" int rt2_render_host(rt2_scene* s, const rt2_uniforms* u, uint32_t fra
     (void)hipFree(res);
     (void)hipFree(acc8);
     return rc;
+}
+
+// Not in rt2.h (diagnostics): counters of the last rt2_scene_stats call
+// [1] segments, [2] groups, [3] groups with survivors, [4] exact iterations,
+// [5] lane survivors (STATS variants only), and the variant last launched.
+extern "C" int rt2_scene_diag(rt2_scene* s, unsigned long long* out8, int* last_variant) {
+    if (!s || !out8) return -1;
+    std::memcpy(out8, s->diag, sizeof(s->diag));
+    if (last_variant) *last_variant = s->last_variant;
+    return 0;
 }
 
 // Not in rt2.h (test hook): exhaustive reciprocal check over [lo, hi] bit patterns.

@@ -29,13 +29,25 @@ scene = rt2.Scene(sd, 0)
 variants = [int(v) for v in a.variants.split(",")]
 times = {v: [] for v in variants}
 ref = None
+import ctypes as C  # noqa: E402
+diag = {}
 for rnd in range(a.rounds):
     for v in variants:
         scene.set_variant(v)
         torch.cuda.synchronize()
+        scene.stats(reset=True)
         t = time.perf_counter()
         img = scene.render_host(u, 0, spec.frames)
         times[v].append(time.perf_counter() - t)
+        scene.stats(reset=True)
+        c = (C.c_ulonglong * 8)()
+        lv = C.c_int()
+        rt2.lib().rt2_scene_diag(scene._p, c, C.byref(lv))
+        if c[2]:
+            diag[v] = dict(segments=c[1], groups=c[2], groups_with_survivor=c[3], exact_iters=c[4],
+                           lane_survivors=c[5], frac_groups_exact=c[3] / c[2], exact_iters_per_group=c[4] / c[2],
+                           lane_survivor_rate=c[5] / (c[2] * 64 * 4),
+                           wave_end_spread_ms=(c[7] - c[6]) * 1e-5 if c[7] > c[6] else None)
         if rnd == 0:
             if ref is None:
                 ref = img
@@ -48,5 +60,4 @@ for v in variants:
     out[rt2.lib().rt2_variant_name(v).decode()] = dict(variant=v, median_ms=round(med * 1e3, 2),
                                                         min_ms=round(min(times[v]) * 1e3, 2),
                                                         msamples_s=round(samples / med / 1e6, 2))
-print(json.dumps({"config": a.config, "W": W, "H": H, "R": R, "segments_per_sample":
-                  st.segments / (samples * a.rounds * len(variants)), "variants": out}, indent=1))
+print(json.dumps({"config": a.config, "W": W, "H": H, "R": R, "variants": out, "diag": diag}, indent=1))

@@ -1,0 +1,63 @@
+"""Summarise rocprofv3 PMC passes (scripts/profile_pmc.sh) for the render kernel.
+
+HBM traffic per launch = (2 * FETCH_SIZE + WRITE_SIZE) KiB -> bytes; FETCH_SIZE is
+doubled per MI355X_MICROARCH.md §HBM (gfx950 reports half the bytes of a wide
+coalesced read; FETCH_SIZE counts Infinity-Cache hits too).  Writes
+profiles/pmc_config<X>.json, which bench.py reads for roofline.traffic.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "gpurun_out")
+
+
+def load(name):
+    files = glob.glob(os.path.join(OUT, f"pmc_{name}", "**", "*counter_collection.csv"), recursive=True)
+    vals = defaultdict(list)  # (kernel, counter) -> per-dispatch values
+    for f in files:
+        per = defaultdict(float)
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                k = row.get("Kernel_Name", "")
+                if "render_" not in k:
+                    continue
+                per[(row["Dispatch_Id"], k, row["Counter_Name"])] += float(row["Counter_Value"])
+        for (disp, k, c), v in per.items():
+            vals[c].append(v)
+    return {c: sum(v) / len(v) for c, v in vals.items() if v}
+
+
+def main(config="B"):
+    res = {}
+    for name in ("fetch", "write", "valu", "salu", "clock", "wait"):
+        res.update(load(name))
+    out = {"config": config, "counters_per_launch": res}
+    if "FETCH_SIZE" in res and "WRITE_SIZE" in res:
+        out["hbm_bytes_per_launch"] = int((2 * res["FETCH_SIZE"] + res["WRITE_SIZE"]) * 1024)
+    trace = glob.glob(os.path.join(OUT, "pmc_clock", "**", "*kernel_trace.csv"), recursive=True)
+    durs = []
+    for f in trace:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if "render_" in row.get("Kernel_Name", ""):
+                    durs.append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+    if durs:
+        out["kernel_ns_profiled"] = sum(durs) / len(durs)
+        if "GRBM_GUI_ACTIVE" in res:
+            out["effective_clock_ghz"] = res["GRBM_GUI_ACTIVE"] / 8 / out["kernel_ns_profiled"]
+    if "SQ_ACTIVE_INST_VALU" in res and "SQ_WAVE_CYCLES" in res:
+        out["valu_active_frac_of_wave_cycles"] = res["SQ_ACTIVE_INST_VALU"] / res["SQ_WAVE_CYCLES"]
+    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+    path = os.path.join(ROOT, "profiles", f"pmc_config{config}.json")
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(*(sys.argv[1:] or ["B"]))

@@ -1,0 +1,19 @@
+#!/bin/bash
+# PMC passes for the bench's render kernel (one counter group per rocprofv3 run,
+# --kernel-trace/--pmc only; no sys/runtime trace).  Output: gpurun_out/pmc_<name>/
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+ARGS="--no-cpu-baseline --steps 2 --warmup 1 ${BENCH_ARGS}"
+run() {
+  local name=$1; shift
+  timeout -k 10 300 rocprofv3 --pmc "$@" --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_$name" -o run \
+    -- python3 "$GRAFT_REPO_ROOT/bench.py" $ARGS > "$GRAFT_REPO_ROOT/gpurun_out/pmc_$name.log" 2>&1
+}
+run fetch FETCH_SIZE && \
+run write WRITE_SIZE && \
+run valu SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES && \
+run salu SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVES && \
+run clock GRBM_GUI_ACTIVE GRBM_COUNT && \
+run wait SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY && \
+echo "pmc ok"
