@@ -36,6 +36,8 @@ VALU_PEAK_TFLOPS = 157.3   # MI355X FP32 vector peak (MI355X_MICROARCH.md, chip-
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec
 FLOP_PER_TEST = 53
 BYTES_PER_TEST = 36        # a, b, c positions
+KERNEL_NAMES = {"brute": "render_smem (rt2_render.hip, variant smem/256/masked8/coop32)",
+                "bvh": "render_bvh (rt2_render.hip, variant bvh/256)"}
 
 
 def parse():
@@ -46,6 +48,8 @@ def parse():
     ap.add_argument("--config", default="B")
     ap.add_argument("--tile-rows", type=int, default=1)
     ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--traversal", default="brute", choices=["brute", "bvh"],
+                    help="brute = the north-star kernel (default); bvh = the reference's traversal on the GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target seconds per CPU baseline mode")
     return ap.parse_args()
@@ -118,6 +122,7 @@ def main():
     sd, spec = rt2.build_config_scene(args.config)
     u = rt2.offline_uniforms(spec.width, spec.height, spec.bounces, spec.rays, sd.num_triangles)
     scene = rt2.Scene(sd, dev)
+    scene.set_traversal(args.traversal)
     if args.variant:
         scene.set_variant(args.variant)
     renderer = rdist.DeviceSlabRenderer(scene, u, 0, spec.frames, args.tile_rows, rank, world)
@@ -190,12 +195,13 @@ def main():
         "data": "synthetic",
         "config": {"workload": f"config {spec.name}: {spec.description}", "width": spec.width,
                    "height": spec.height, "rays_per_pixel": spec.rays, "frames": spec.frames,
-                   "max_bounce": spec.bounces, "triangles": sd.num_triangles, "traversal": "brute force",
+                   "max_bounce": spec.bounces, "triangles": sd.num_triangles,
+                   "traversal": "brute force" if args.traversal == "brute" else "BVH (compute.glsl:410-460)",
                    "seed": "x + y*W + frame*968824447", "parallelism": f"row-tile x{world}" if world > 1 else "1 GPU",
                    "tile_rows": args.tile_rows},
         "roofline": {"bound": "valu", "achieved": round(flops, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(flops / VALU_PEAK_TFLOPS, 4), "traffic": None,
-                     "kernel": "render_smem (rt2_render.hip, variant smem/256/masked8/coop32)", "kernel_ms": round(kern_ms, 3),
+                     "kernel": KERNEL_NAMES[args.traversal], "kernel_ms": round(kern_ms, 3),
                      "tests_per_launch": int(tests_per_launch),
                      "segments_per_sample": round(segs / (samples_per_step * args.steps), 4),
                      "hbm_read_algorithmic": {"achieved": round(hbm_read, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -196,6 +196,14 @@ int rt2_scene_stats(rt2_scene* scene, rt2_stats* out, int reset);
  * next render will use for this scene. */
 int rt2_scene_set_variant(rt2_scene* scene, int variant);
 
+/* Closest-hit algorithm.  BRUTE (default): every triangle in array order, the
+ * north-star kernel.  BVH: the reference's own traversal of the node array
+ * (calculateRayCollisionBVH, compute.glsl:410-460; needs `nodes` at
+ * rt2_scene_create) — identical to BRUTE except on exact distance ties, where
+ * it resolves in the reference's visiting order. */
+enum { RT2_TRAVERSAL_BRUTE = 0, RT2_TRAVERSAL_BVH = 1 };
+int rt2_scene_set_traversal(rt2_scene* scene, int traversal);
+
 /* ------------------------------------------------------------------------
  * (2) Host surface
  * ---------------------------------------------------------------------- */

@@ -55,6 +55,8 @@ struct RenderParams {
     unsigned long long* item_counter;
     unsigned long long* seg_counter;
     int tile_tris;  // TILED: triangles per LDS tile
+    const rt2_node* nodes;  // BVH traversal
+    int stack_slots;        // BVH: per-lane stack entries (tree depth + 2)
 };
 
 enum : int { ST_NEED_ITEM = 0, ST_NEW_FRAME = 1, ST_NEW_RAY = 2, ST_TRACE = 3, ST_DONE = 4 };
@@ -763,6 +765,105 @@ __global__ __launch_bounds__(BLOCK) void render_smem(RenderParams p) {
     flush_counters(L, p);
 }
 
+// ---------------------------------------------------------------------------
+// BVH traversal: calculateRayCollisionBVH, compute.glsl:410-460, per lane.
+// Stack in LDS (slot-major [slot][thread]: conflict-free), near child pushed
+// last so it is popped first, far/near pushed only if their box distance is
+// below the running best — the reference's visiting order exactly, so ties
+// resolve as in the reference (and as the oracle's bvh mode).
+// ---------------------------------------------------------------------------
+
+// rayBoundsIntersect, compute.glsl:382-408.  The per-axis early return is
+// folded into one final test: tMin only grows and tMax only shrinks, so a
+// failed check stays failed (and |d| = 1 guarantees an unskipped axis).
+__device__ __forceinline__ float ray_bounds(const f3& o, const f3& d, bool sx, bool sy, bool sz, const float* bmin,
+                                            const float* bmax) {
+    float tMin = -1e32f, tMax = 1e32f;
+    if (!sx) {
+        float t0 = (bmin[0] - o.x) / d.x, t1 = (bmax[0] - o.x) / d.x;
+        if (t0 > t1) { const float t = t0; t0 = t1; t1 = t; }
+        if (tMin < t0) tMin = t0;
+        if (tMax > t1) tMax = t1;
+    }
+    if (!sy) {
+        float t0 = (bmin[1] - o.y) / d.y, t1 = (bmax[1] - o.y) / d.y;
+        if (t0 > t1) { const float t = t0; t0 = t1; t1 = t; }
+        if (tMin < t0) tMin = t0;
+        if (tMax > t1) tMax = t1;
+    }
+    if (!sz) {
+        float t0 = (bmin[2] - o.z) / d.z, t1 = (bmax[2] - o.z) / d.z;
+        if (t0 > t1) { const float t = t0; t0 = t1; t1 = t; }
+        if (tMin < t0) tMin = t0;
+        if (tMax > t1) tMax = t1;
+    }
+    return (tMin >= tMax || tMax < 0.0f) ? 1e38f : tMin;
+}
+
+template <int BLOCK>
+__device__ __forceinline__ void closest_bvh(const f3& o, const f3& d, const rt2_node* __restrict__ nodes,
+                                            const float4* __restrict__ tri, int* stack, int stack_slots,
+                                            float& best, int& bi, uint32_t& tests) {
+    const bool sx = d.x < 1e-6f && d.x > -1e-6f;
+    const bool sy = d.y < 1e-6f && d.y > -1e-6f;
+    const bool sz = d.z < 1e-6f && d.z > -1e-6f;
+    float bestK = best * 1.0009765625f;
+    int* st = stack + threadIdx.x;
+    int sp = 0;
+    st[0] = 0;
+    sp = 1;
+    while (sp > 0) {
+        sp -= 1;
+        const int ni = st[sp * BLOCK];
+        const int4 meta = *reinterpret_cast<const int4*>(&nodes[ni].triangleIndex);
+        if (meta.z == -1) {  // leaf: compute.glsl:429-435
+            tests += (uint32_t)max(meta.y, 0);
+            for (int i = meta.x; i < meta.x + meta.y; i++) {
+                const float4* t = tri + 3 * i;
+                const MtQ q = mt_quantities(o, d, t[0], t[1], t[2]);
+                if (mt_pass(q, bestK)) mt_exact(q, i, best, bi, bestK);
+            }
+        } else {  // compute.glsl:441-456
+            const int ia = meta.z, ib = meta.z + 1;
+            const float dA = ray_bounds(o, d, sx, sy, sz, nodes[ia].bmin, nodes[ia].bmax);
+            const float dB = ray_bounds(o, d, sx, sy, sz, nodes[ib].bmin, nodes[ib].bmax);
+            const bool nearA = dA < dB;
+            const float dNear = nearA ? dA : dB;
+            const float dFar = nearA ? dB : dA;
+            const int iNear = nearA ? ia : ib;
+            const int iFar = nearA ? ib : ia;
+            if (dFar < best && sp < stack_slots) st[(sp++) * BLOCK] = iFar;
+            if (dNear < best && sp < stack_slots) st[(sp++) * BLOCK] = iNear;
+        }
+    }
+}
+
+// BVH: per-lane traversal of the reference's node array (nodes uploaded with
+// the scene).  Dynamic LDS = stack_slots * BLOCK ints.
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void render_bvh(RenderParams p) {
+    extern __shared__ int bvh_stack[];
+    Lane L;
+    lane_init(L);
+    uint32_t tests = 0;
+    for (;;) {
+        advance(L, p);
+        if (!__any(L.st == ST_TRACE)) break;
+        if (L.st == ST_TRACE) {
+            L.bounce += 1;
+            L.segs += 1;
+            float best = 1e38f;
+            int bi = -1;
+            closest_bvh<BLOCK>(L.o, L.d, p.nodes, p.tri, bvh_stack, p.stack_slots, best, bi, tests);
+            shade(L, p, best, bi);
+        }
+    }
+    flush_counters(L, p);
+    unsigned long long t = tests;
+    for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+    if (lane_id() == 0) atomicAdd(p.seg_counter + 1, t);  // leaf triangle tests
+}
+
 // Pre-transform: RTXTriangle (80 B) -> {a, e0, e1, n} (48 B) + material index.
 __global__ void prep_triangles(const rt2_triangle* tris, int n, float4* out, int* mtl) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -855,10 +956,68 @@ struct rt2_scene {
     unsigned long long samples = 0, tests_per_seg = 0;
     int variant = 0;
     int last_variant = -1;
+    int traversal = RT2_TRAVERSAL_BRUTE;
+    int bvh_depth = 0;              // longest root-to-leaf path (nodes)
+    int last_kind = 0;              // kind of the last launch (stats: tests)
     unsigned long long diag[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int num_cus = 256;
     size_t max_lds = 65536;
 };
+
+// Validates a reference node array (BVH.h layout) against the triangle count
+// and returns its depth; < 0 on a malformed array (child out of range, cycle,
+// leaf range outside the triangles).
+static int bvh_depth_check(const rt2_node* nodes, int n_nodes, int n_tris, std::string& err) {
+    if (n_nodes < 1) {
+        err = "empty node array";
+        return -1;
+    }
+    std::vector<int> depth(n_nodes, 0);
+    std::vector<int> stack;
+    stack.push_back(0);
+    depth[0] = 1;
+    int maxd = 1;
+    long long visited = 0;
+    while (!stack.empty()) {
+        const int i = stack.back();
+        stack.pop_back();
+        if (++visited > n_nodes) {
+            err = "node graph is not a tree";
+            return -1;
+        }
+        const rt2_node& n = nodes[i];
+        if (n.childIndex == -1) {
+            if (n.triangleCount > 0 && (n.triangleIndex < 0 || (long long)n.triangleIndex + n.triangleCount > n_tris)) {
+                err = "leaf " + std::to_string(i) + " references triangles outside [0, " + std::to_string(n_tris) + ")";
+                return -1;
+            }
+            continue;
+        }
+        if (n.childIndex <= 0 || n.childIndex + 1 >= n_nodes) {
+            err = "node " + std::to_string(i) + " has child index " + std::to_string(n.childIndex) + " out of range";
+            return -1;
+        }
+        for (int c = n.childIndex; c <= n.childIndex + 1; c++) {
+            depth[c] = depth[i] + 1;
+            maxd = std::max(maxd, depth[c]);
+            stack.push_back(c);
+        }
+    }
+    return maxd;
+}
+
+extern "C" int rt2_scene_set_traversal(rt2_scene* s, int traversal) {
+    if (!s || (traversal != RT2_TRAVERSAL_BRUTE && traversal != RT2_TRAVERSAL_BVH)) {
+        rt2h::set_error("rt2_scene_set_traversal: bad argument");
+        return -1;
+    }
+    if (traversal == RT2_TRAVERSAL_BVH && s->n_nodes == 0) {
+        rt2h::set_error("rt2_scene_set_traversal: BVH traversal needs the node array (rt2_scene_create nodes)");
+        return -1;
+    }
+    s->traversal = traversal;
+    return 0;
+}
 
 extern "C" int rt2_scene_create(const rt2_triangle* tris, int32_t n_tris, const rt2_material* mats, int32_t n_mats,
                                 const rt2_node* nodes, int32_t n_nodes, int32_t device, rt2_scene** out) {
@@ -899,6 +1058,14 @@ extern "C" int rt2_scene_create(const rt2_triangle* tris, int32_t n_tris, const 
     if (n_tris > 0) HIPCHECK(hipMemcpy(s->d_raw, tris, (size_t)n_tris * sizeof(rt2_triangle), hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(s->d_mats, mats, (size_t)n_mats * sizeof(rt2_material), hipMemcpyHostToDevice));
     if (s->n_nodes > 0) {
+        std::string err;
+        s->bvh_depth = bvh_depth_check(nodes, n_nodes, n_tris, err);
+        if (s->bvh_depth < 0 || s->bvh_depth > 62) {
+            if (s->bvh_depth > 62) err = "BVH deeper than compute.glsl's 64-entry stack";
+            rt2h::set_error("rt2_scene_create: bad node array: " + err);
+            delete s;
+            return -1;
+        }
         HIPCHECK(hipMalloc(&s->d_nodes, (size_t)n_nodes * sizeof(rt2_node)));
         HIPCHECK(hipMemcpy(s->d_nodes, nodes, (size_t)n_nodes * sizeof(rt2_node), hipMemcpyHostToDevice));
     }
@@ -947,7 +1114,7 @@ namespace {
 constexpr int kTileTris = 1024;  // 48 KiB of LDS per tile
 
 // Kernel variants (rt2_scene_set_variant); 0 = auto = the default below.
-enum Kind : int { K_RESIDENT = 0, K_TILED = 1, K_SMEM = 2 };
+enum Kind : int { K_RESIDENT = 0, K_TILED = 1, K_SMEM = 2, K_BVH = 3 };
 struct Variant {
     int kind;
     int block;
@@ -962,6 +1129,8 @@ hipError_t launch_t(const RenderParams& p, int blocks, size_t lds, hipStream_t s
         hipLaunchKernelGGL((render_tiled<BLOCK, MT, UNROLL>), dim3(blocks), dim3(BLOCK), lds, st, p);
     else if constexpr (KIND == K_SMEM)
         hipLaunchKernelGGL((render_smem<BLOCK, MT % 1000, MT / 1000>), dim3(blocks), dim3(BLOCK), 0, st, p);
+    else if constexpr (KIND == K_BVH)
+        hipLaunchKernelGGL((render_bvh<BLOCK>), dim3(blocks), dim3(BLOCK), lds, st, p);
     else
         hipLaunchKernelGGL((render_resident<BLOCK, MT, UNROLL>), dim3(blocks), dim3(BLOCK), lds, st, p);
     return hipGetLastError();
@@ -972,6 +1141,8 @@ hipError_t occ_t(int* occ, size_t lds) {
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_tiled<BLOCK, MT, UNROLL>, BLOCK, lds);
     else if constexpr (KIND == K_SMEM)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_smem<BLOCK, MT % 1000, MT / 1000>, BLOCK, 0);
+    else if constexpr (KIND == K_BVH)
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_bvh<BLOCK>, BLOCK, lds);
     else
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_resident<BLOCK, MT, UNROLL>, BLOCK, lds);
 }
@@ -1015,10 +1186,14 @@ const Variant kVariants[] = {
     RT2_VARIANT(K_RESIDENT, 1024, 204, 1, "resident/1024/lean4"),    // 34
     RT2_VARIANT(K_RESIDENT, 512, 208, 1, "resident/512/lean8"),      // 35
     RT2_VARIANT(K_SMEM, 512, 208, 1, "smem/512/lean8"),              // 36
+    RT2_VARIANT(K_BVH, 256, 0, 1, "bvh/256"),                        // 37: default (BVH traversal)
+    RT2_VARIANT(K_BVH, 128, 0, 1, "bvh/128"),                        // 38
+    RT2_VARIANT(K_BVH, 512, 0, 1, "bvh/512"),                        // 39
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr size_t kResidentMaxBytes = 112 * 1024;
 constexpr int kSmemMaxTris = 16384;
+constexpr int kDefaultBvhVariant = 37;
 }  // namespace
 
 extern "C" const char* rt2_variant_name(int v) { return v >= 0 && v < kNumVariants ? kVariants[v].name : nullptr; }
@@ -1095,11 +1270,23 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     int vi = s->variant;
     // auto: scalar-path kernel for small scenes (config B: 1,208 triangles),
     // LDS-tiled sweep for large ones (config C/E: 100k-1M triangles)
-    if (vi <= 0 || vi >= kNumVariants) vi = s->n_tris <= kSmemMaxTris ? 0 : 2;
-    if (kVariants[vi].kind == K_RESIDENT && !fits) vi = 2;  // a resident variant cannot hold this scene
+    if (s->traversal == RT2_TRAVERSAL_BVH) {
+        if (vi <= 0 || vi >= kNumVariants || kVariants[vi].kind != K_BVH) vi = kDefaultBvhVariant;
+    } else {
+        if (vi <= 0 || vi >= kNumVariants || kVariants[vi].kind == K_BVH) vi = s->n_tris <= kSmemMaxTris ? 0 : 2;
+        if (kVariants[vi].kind == K_RESIDENT && !fits) vi = 2;  // a resident variant cannot hold this scene
+    }
     const Variant& V = kVariants[vi];
-    const size_t lds = V.kind == K_TILED ? (size_t)3 * sizeof(float4) * kTileTris
-                                         : (V.kind == K_SMEM ? 0 : resident_bytes);
+    p.nodes = s->d_nodes;
+    p.stack_slots = s->bvh_depth + 2;
+    size_t lds = 0;
+    if (V.kind == K_TILED)
+        lds = (size_t)3 * sizeof(float4) * kTileTris;
+    else if (V.kind == K_RESIDENT)
+        lds = resident_bytes;
+    else if (V.kind == K_BVH)
+        lds = (size_t)p.stack_slots * V.block * sizeof(int);
+    s->last_kind = V.kind;
     int occ = 0;
     HIPCHECK(V.occupancy(&occ, lds));
     occ = std::max(occ, 1);
@@ -1126,7 +1313,9 @@ extern "C" int rt2_scene_stats(rt2_scene* s, rt2_stats* out, int reset) {
     std::memcpy(s->diag, c, sizeof(c));
     out->samples = s->samples;
     out->segments = c[1];
-    out->tests = c[1] * (unsigned long long)s->n_tris;
+    // brute force tests every triangle per segment; the BVH kernel counts its
+    // leaf tests in c[2]
+    out->tests = s->last_kind == 3 ? c[2] : c[1] * (unsigned long long)s->n_tris;
     if (reset) {
         s->samples = 0;
         HIPCHECK(hipMemset(s->d_counters, 0, sizeof(c)));

@@ -139,7 +139,7 @@ assert TRI_DTYPE.itemsize == 80 and MAT_DTYPE.itemsize == 96 and NODE_DTYPE.item
 EXPORTED = [
     "rt2_last_error", "rt2_abi_version", "rt2_scene_create", "rt2_scene_destroy", "rt2_shard_rows",
     "rt2_shard_row", "rt2_render", "rt2_render_host", "rt2_resolve_rgba32f", "rt2_resolve_rgb8_reference",
-    "rt2_scene_stats", "rt2_scene_set_variant", "rt2_sd_create", "rt2_sd_destroy", "rt2_sd_load_obj_folder",
+    "rt2_scene_stats", "rt2_scene_set_variant", "rt2_scene_set_traversal", "rt2_sd_create", "rt2_sd_destroy", "rt2_sd_load_obj_folder",
     "rt2_sd_add_material", "rt2_sd_add_triangle", "rt2_sd_add_triangles", "rt2_sd_add_cornell_box", "rt2_sd_add_mirror_cornell_box",
     "rt2_sd_add_side_lit_cornell_box", "rt2_sd_add_sky_light_plane", "rt2_sd_add_cube",
     "rt2_sd_create_classic_cornell_box", "rt2_sd_create_diverse_cornell_box", "rt2_sd_build_bvh",
@@ -191,6 +191,7 @@ def lib() -> C.CDLL:
         "rt2_resolve_rgb8_reference": (C.c_int, [P, I64, U32, P]),
         "rt2_scene_stats": (C.c_int, [P, C.POINTER(Stats), C.c_int]),
         "rt2_scene_set_variant": (C.c_int, [P, C.c_int]),
+        "rt2_scene_set_traversal": (C.c_int, [P, C.c_int]),
         "rt2_sd_create": (P, []),
         "rt2_sd_destroy": (None, [P]),
         "rt2_sd_load_obj_folder": (C.c_int, [P, C.c_char_p]),
@@ -407,6 +408,10 @@ class Scene:
 
     def set_variant(self, v: int) -> int:
         return lib().rt2_scene_set_variant(self._p, v)
+
+    def set_traversal(self, traversal: str) -> None:
+        """"brute" (north-star kernel) or "bvh" (compute.glsl:410-460 on the uploaded nodes)."""
+        _check(lib().rt2_scene_set_traversal(self._p, {"brute": 0, "bvh": 1}[traversal]), "set_traversal")
 
     def render(self, u: Uniforms, frame_begin: int, frame_count: int, sh: Shard, accum_ptr: int,
                accum8_ptr: int = 0, stream: int = 0) -> None:
