@@ -18,9 +18,10 @@ Prints ONE JSON line (rank 0):
               launch's average HIP-event duration, against 157.3 TFLOP/s; plus
               the north star's HBM-read figure (36 B x tests) against 8 TB/s
   cpu_baseline  the CPU restatement of compute.glsl (oracle/, reference-faithful
-              BVH traversal) on the host cores, on a bounded strided row sample;
-              the brute-force CPU rate is reported beside it
-  parity      GPU rows vs the CPU oracle on those same sampled rows
+              BVH traversal) on the host cores, on a bounded strided pixel sample
+              (every k-th pixel in raster order, full spp); the brute-force CPU
+              rate is reported beside it
+  parity      GPU pixels vs the CPU oracle on those same sampled pixels
 """
 import argparse
 import json
@@ -37,7 +38,7 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec
 FLOP_PER_TEST = 53
 BYTES_PER_TEST = 36        # a, b, c positions
 KERNEL_NAMES = {"brute": "render_smem (rt2_render.hip, variant smem/256/masked8/coop32)",
-                "bvh": "render_bvh (rt2_render.hip, variant bvh/256)"}
+                "bvh": "render_bvh2 (rt2_render.hip, variant bvh2/256/t16)"}
 
 
 def parse():
@@ -56,47 +57,49 @@ def parse():
 
 
 def cpu_baseline(sd, spec, u, gpu_image, threads):
-    """Times oracle/ (CPU restatement of compute.glsl) on a strided row sample and
-    checks the GPU's rows against it.  Test infrastructure: the oracle is only the
-    checker / baseline here, never the measured path."""
+    """Times oracle/ (CPU restatement of compute.glsl) on a strided pixel sample
+    (every k-th pixel in raster order, full spp) and checks the GPU's pixels
+    against it.  Test infrastructure: the oracle is only the checker / baseline
+    here, never the measured path."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle
     tris, mats, nodes = sd.triangles(), sd.materials(), sd.nodes()
     H, W = spec.height, spec.width
+    npx_all = H * W
     res = {}
-    rows_done = {}
+    done = {}
     for mode in ("bvh", "brute"):
-        # calibrate on a few spread rows, then size the sample to ~cpu_seconds
-        probe = np.linspace(H // 16, H - 1 - H // 16, 4).astype(np.int32)
-        if mode == "brute":
-            probe = probe[1:3]
+        # calibrate on a spread probe, then size the sample to ~cpu_seconds
+        nprobe = 4 * threads
+        pid = np.linspace(npx_all // 7, npx_all - 1 - npx_all // 7, nprobe).astype(np.int64)
         t0 = time.perf_counter()
-        oracle.render(tris, mats, u, probe, 0, spec.frames, mode, nodes=nodes, threads=threads)
-        dt = max(time.perf_counter() - t0, 1e-3) / len(probe)
-        nrows = int(max(1, min(H, args.cpu_seconds / dt)))
-        stride = max(1, H // nrows)
-        rows = np.arange(stride // 2, H, stride, dtype=np.int32)[:nrows]
+        oracle.render_pixels(tris, mats, u, pid % W, pid // W, 0, spec.frames, mode, nodes=nodes, threads=threads)
+        dt = max(time.perf_counter() - t0, 1e-3) / nprobe
+        n = int(max(threads, min(npx_all, args.cpu_seconds / dt)))
+        stride = max(1, npx_all // n)
+        pid = np.arange(stride // 2, npx_all, stride, dtype=np.int64)[:n]
+        xs, ys = pid % W, pid // W
         t0 = time.perf_counter()
-        acc, _, segs, tests = oracle.render(tris, mats, u, rows, 0, spec.frames, mode, nodes=nodes,
-                                            threads=threads)
+        acc, _, segs, tests = oracle.render_pixels(tris, mats, u, xs, ys, 0, spec.frames, mode, nodes=nodes,
+                                                   threads=threads)
         dt = time.perf_counter() - t0
-        samples = len(rows) * W * spec.rays * spec.frames
-        res[mode] = dict(value=samples / dt / 1e6, rows=len(rows), stride=stride, seconds=dt,
+        samples = len(pid) * spec.rays * spec.frames
+        res[mode] = dict(value=samples / dt / 1e6, pixels=int(len(pid)), stride=int(stride), seconds=dt,
                          segments_per_sample=segs / samples, tests_per_segment=tests / max(segs, 1))
-        rows_done[mode] = (rows, acc / spec.frames)
+        done[mode] = (ys, xs, acc / spec.frames)
     parity = None
     if gpu_image is not None:
-        rows, ref = rows_done["brute"]
-        g = gpu_image[rows][..., :3]
-        d = np.abs(g - ref[..., :3])
-        rows_b, ref_b = rows_done["bvh"]
-        db = np.abs(gpu_image[rows_b][..., :3] - ref_b[..., :3])
-        parity = dict(rows=int(len(rows) + len(rows_b)), oracle_modes=["brute", "bvh"],
-                      exact_pixel_frac_brute=float((d.max(-1) == 0).mean()),
-                      exact_pixel_frac_bvh=float((db.max(-1) == 0).mean()),
-                      rmse=float(np.sqrt(np.concatenate([(d ** 2).ravel(), (db ** 2).ravel()]).mean())),
-                      max_abs=float(max(d.max(), db.max())), tolerance_rmse=1e-4)
+        ds = []
+        fr = {}
+        for mode, (ys, xs, ref) in done.items():
+            d = np.abs(gpu_image[ys, xs][..., :3] - ref[..., :3])
+            ds.append(d)
+            fr[mode] = float((d.max(-1) == 0).mean())
+        parity = dict(pixels=int(sum(len(d) for d in ds)), oracle_modes=list(done),
+                      exact_pixel_frac_brute=fr["brute"], exact_pixel_frac_bvh=fr["bvh"],
+                      rmse=float(np.sqrt(np.concatenate([(d ** 2).ravel() for d in ds]).mean())),
+                      max_abs=float(max(d.max() for d in ds)), tolerance_rmse=1e-4)
     return res, parity
 
 
@@ -219,10 +222,12 @@ def main():
         res, parity = cpu_baseline(sd, spec, u, gpu_np, threads)
         out["cpu_baseline"] = {"value": round(res["bvh"]["value"], 4), "unit": "Msamples/s", "cores": threads,
                                "kind": "port",
-                               "sample": f"rows y = {res['bvh']['stride'] // 2} + {res['bvh']['stride']}k "
-                                         f"({res['bvh']['rows']} of {spec.height} rows), full spp, reference BVH "
-                                         f"traversal (compute.glsl:410-460), {res['bvh']['seconds']:.1f} s",
-                               "brute_force": {"value": round(res["brute"]["value"], 4), "rows": res["brute"]["rows"],
+                               "sample": f"pixels i = {res['bvh']['stride'] // 2} + {res['bvh']['stride']}k in raster "
+                                         f"order ({res['bvh']['pixels']} of {spec.width * spec.height}), full spp, "
+                                         f"reference BVH traversal (compute.glsl:410-460), "
+                                         f"{res['bvh']['seconds']:.1f} s",
+                               "brute_force": {"value": round(res["brute"]["value"], 4),
+                                               "pixels": res["brute"]["pixels"],
                                                "seconds": round(res["brute"]["seconds"], 2)},
                                "gpu_over_cpu_bvh": round(value / res["bvh"]["value"], 1),
                                "gpu_over_cpu_brute": round(value / res["brute"]["value"], 1)}

@@ -164,8 +164,10 @@ int32_t rt2_shard_row(int32_t local_row, rt2_shard shard);
  * d_accum8 (nullable, device, rows*W*4 uint32) accumulates the per-frame GL
  * unorm8 quantisation of the same colours — the reference screenshot path
  * (rayTracing.cpp:217-238).  `stream` is a hipStream_t (NULL = default);
- * the call is asynchronous like glDispatchCompute.  uniforms->basicShading
- * must be 0 (the one-ray preview traceBasic is not on this path). */
+ * the call is asynchronous like glDispatchCompute.  uniforms->basicShading != 0
+ * selects the one-ray preview (traceBasic, compute.glsl:565-645 and the
+ * basicShading branch of main, :672-678): deterministic, no jitter, no
+ * tonemap; numRaysPerPixel is then ignored. */
 int rt2_render(rt2_scene* scene, const rt2_uniforms* uniforms,
                uint32_t frame_begin, uint32_t frame_count, rt2_shard shard,
                float* d_accum, uint32_t* d_accum8, void* stream);

@@ -32,6 +32,9 @@ def lib() -> C.CDLL:
         L.oracle_render.restype = C.c_int
         L.oracle_render.argtypes = [P, C.c_int32, P, C.c_int32, P, C.c_int32, P, C.c_uint32, C.c_uint32, P,
                                     C.c_int32, C.c_int32, C.c_int32, P, P, P, P]
+        L.oracle_render_pixels.restype = C.c_int
+        L.oracle_render_pixels.argtypes = [P, C.c_int32, P, C.c_int32, P, C.c_int32, P, C.c_uint32, C.c_uint32, P,
+                                           C.c_int64, C.c_int32, C.c_int32, P, P, P, P]
         L.oracle_pcg_next.restype = C.c_uint32
         L.oracle_pcg_next.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_float)]
         L.oracle_ray_triangle.restype = C.c_int
@@ -69,6 +72,32 @@ def render(triangles: np.ndarray, materials: np.ndarray, uniforms, rows, frame_b
                              None if acc8 is None else acc8.ctypes.data, C.byref(segs), C.byref(tests))
     if rc != 0:
         raise RuntimeError(f"oracle_render failed: {rc}")
+    return acc, acc8, segs.value, tests.value
+
+
+def render_pixels(triangles: np.ndarray, materials: np.ndarray, uniforms, xs, ys, frame_begin: int = 0,
+                  frame_count: int = 1, mode: str = "brute", nodes: np.ndarray | None = None,
+                  threads: int | None = None, with_acc8: bool = False):
+    """Renders the pixels (xs[i], ys[i]).  Returns (accum[n, 4] = per-pixel SUM over
+    frames, acc8 or None, segments, tests)."""
+    tri = np.ascontiguousarray(triangles)
+    mat = np.ascontiguousarray(materials)
+    assert tri.dtype.itemsize == 80 and mat.dtype.itemsize == 96
+    px = np.ascontiguousarray(np.stack([np.asarray(xs, np.int32), np.asarray(ys, np.int32)], -1))
+    n = len(px)
+    acc = np.zeros((n, 4), dtype=np.float32)
+    acc8 = np.zeros((n, 4), dtype=np.uint32) if with_acc8 else None
+    segs = C.c_uint64(0)
+    tests = C.c_uint64(0)
+    nd = None if nodes is None else np.ascontiguousarray(nodes)
+    m = {"brute": 0, "bvh": 1}[mode]
+    rc = lib().oracle_render_pixels(tri.ctypes.data, len(tri), mat.ctypes.data, len(mat),
+                                    None if nd is None else nd.ctypes.data, 0 if nd is None else len(nd),
+                                    C.addressof(uniforms), frame_begin, frame_count, px.ctypes.data, n, m,
+                                    threads or os.cpu_count() or 1, acc.ctypes.data,
+                                    None if acc8 is None else acc8.ctypes.data, C.byref(segs), C.byref(tests))
+    if rc != 0:
+        raise RuntimeError(f"oracle_render_pixels failed: {rc}")
     return acc, acc8, segs.value, tests.value
 
 

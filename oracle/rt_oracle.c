@@ -337,6 +337,86 @@ static v3 trace(const ctx_t* c, v3 origin, v3 dir, uint32_t* rng, uint64_t* segs
     return incomingLight;
 }
 
+/* normalizeColor, compute.glsl:462-470 */
+static inline v3 normalize_color(v3 c) {
+    float m = fmaxf(fmaxf(c.x, c.y), c.z);
+    if (m > 1.0f) return divs(c, m);
+    return c;
+}
+
+/* traceBasic, compute.glsl:565-645 — the interactive one-ray preview.  `Ray
+ * ray;` leaves insideGlass uninitialised in the shader (:674); it starts false
+ * here.  TEXTURE samples nothing (no textures bound), as in trace(). */
+static v3 trace_basic(const ctx_t* c, v3 origin, v3 dir, uint64_t* segs, uint64_t* tests) {
+    v3 colorCumulative = mk(0.0f, 0.0f, 0.0f);
+    int insideGlass = 0;
+    int bounceCount = 0;
+    while (bounceCount < c->u->maxBounceCount) {
+        bounceCount++;
+        *segs += 1;
+        hit_t h = closest(c, origin, dir, tests);
+        if (h.didHit) {
+            const oracle_triangle* t = &c->tris[h.tri];
+            v3 a = v4xyz(t->a), b = v4xyz(t->b), cc = v4xyz(t->c);
+            v3 normal = normalize(cross(sub(b, a), sub(cc, a)));
+            v3 hitPoint = add(origin, muls(dir, h.dst));
+            origin = sub(hitPoint, muls(normal, 1e-4f));
+            const oracle_material* m = &c->mats[t->materialIndex];
+            switch (m->materialType) {
+            case SPECULAR:
+                colorCumulative = add(colorCumulative, v4xyz(m->color));
+                dir = reflect(dir, normal);
+                break;
+            case DIFFUSE:
+            case TEXTURE:
+            case CHECKER: {
+                v3 color;
+                if (m->materialType == TEXTURE) {
+                    color = mk(0.0f, 0.0f, 0.0f);
+                } else if (m->materialType == DIFFUSE) {
+                    color = v4xyz(m->color);
+                } else {
+                    float s = m->checkerScale;
+                    int black = 0;
+                    if (s > 0.0f) {
+                        float sum = floorf(origin.x * s) + floorf(origin.y * s) + floorf(origin.z * s);
+                        black = (sum - 2.0f * floorf(sum / 2.0f)) == 0.0f;
+                    }
+                    color = black ? mk(0.0f, 0.0f, 0.0f) : mk(1.0f, 1.0f, 1.0f);
+                }
+                colorCumulative = add(colorCumulative, color);
+                if (c->u->basicShadingShadow) {
+                    v3 toLight = normalize(sub(v4xyz(c->u->basicShadingLightPosition), hitPoint));
+                    *segs += 1;
+                    hit_t h2 = closest(c, origin, toLight, tests);
+                    v3 r = h2.didHit ? divs(colorCumulative, 5.0f) : colorCumulative;
+                    return divs(r, (float)bounceCount);
+                }
+                return divs(colorCumulative, (float)bounceCount);
+            }
+            case LIGHT:
+                return normalize_color(v4xyz(m->emissionColor));
+            case GLASS: {
+                float eta = insideGlass ? m->refractiveIndex : 1.0f / m->refractiveIndex;
+                int isRefracted;
+                dir = refract_(dir, normal, eta, &isRefracted);
+                insideGlass = isRefracted != insideGlass;
+                colorCumulative = v4xyz(m->color);
+                break;
+            }
+            case GLASS_HIGHLIGHT:
+                break; /* `if (bounceCount == 0)` never holds after bounceCount++ */
+            default:
+                return mk(1.0f, 0.0f, 1.0f);
+            }
+        } else {
+            colorCumulative = add(colorCumulative, sky(dir));
+            break;
+        }
+    }
+    return divs(colorCumulative, (float)bounceCount);
+}
+
 /* tonemapACES + toSRGB, compute.glsl:647-658 */
 static inline float aces1(float x) {
     const float a = 2.51f, b = 0.03f, cc = 2.43f, d = 0.59f, e = 0.14f;
@@ -352,6 +432,11 @@ static v3 render_pixel_frame(const ctx_t* c, int tx, int ty, uint32_t frame, uin
     float y = (float)(ty * 2 - H) / (float)H;
     uint32_t seed = (uint32_t)tx + (uint32_t)ty * (uint32_t)W + frame * 968824447u;
     v3 cam = v4xyz(u->cameraPos);
+    if (u->basicShading) { /* compute.glsl:672-678: no jitter, no RNG, no tonemap */
+        v3 dir = normalize(add(add(v4xyz(u->viewportFront), muls(v4xyz(u->viewportRight), x)),
+                               muls(v4xyz(u->viewportUp), y)));
+        return trace_basic(c, cam, dir, segs, tests);
+    }
     v3 endPoint = add(add(add(cam, v4xyz(u->viewportFront)), muls(v4xyz(u->viewportRight), x)),
                       muls(v4xyz(u->viewportUp), y));
     v3 colorCumulative = mk(0.0f, 0.0f, 0.0f);
@@ -372,30 +457,26 @@ static v3 render_pixel_frame(const ctx_t* c, int tx, int ty, uint32_t frame, uin
 /* ---- threaded driver ----------------------------------------------------- */
 typedef struct {
     const ctx_t* c;
-    const int32_t* rows;
-    int32_t n_rows;
+    const int32_t* px; /* (x, y) pairs */
+    int64_t n_px;
     uint32_t frame_begin, frame_count;
     float* out_rgba;
     uint32_t* out_acc8;
-    atomic_int next_row;
+    atomic_llong next_unit;
     atomic_ullong segs, tests;
 } job_t;
 
 static void* worker(void* arg) {
     job_t* j = (job_t*)arg;
     const ctx_t* c = j->c;
-    int W = (int)c->u->width;
     uint64_t segs = 0, tests = 0;
-    const int chunk = 32; /* work unit: 32 pixels of one row */
-    const int per_row = (W + chunk - 1) / chunk;
+    const int64_t chunk = 32; /* work unit: 32 consecutive list pixels */
     for (;;) {
-        int unit = atomic_fetch_add(&j->next_row, 1);
-        if (unit >= j->n_rows * per_row) break;
-        int r = unit / per_row;
-        int ty = j->rows[r];
-        int x0 = (unit % per_row) * chunk;
-        int x1 = x0 + chunk < W ? x0 + chunk : W;
-        for (int tx = x0; tx < x1; tx++) {
+        int64_t p0 = atomic_fetch_add(&j->next_unit, 1) * chunk;
+        if (p0 >= j->n_px) break;
+        int64_t p1 = p0 + chunk < j->n_px ? p0 + chunk : j->n_px;
+        for (int64_t p = p0; p < p1; p++) {
+            const int tx = j->px[2 * p], ty = j->px[2 * p + 1];
             float acc[3] = {0.0f, 0.0f, 0.0f};
             uint32_t a8[3] = {0, 0, 0};
             for (uint32_t f = 0; f < j->frame_count; f++) {
@@ -410,7 +491,7 @@ static void* worker(void* arg) {
                     a8[k] += (uint32_t)q;
                 }
             }
-            size_t o = ((size_t)r * (size_t)W + (size_t)tx) * 4;
+            size_t o = (size_t)p * 4;
             if (j->out_rgba) {
                 j->out_rgba[o + 0] = acc[0];
                 j->out_rgba[o + 1] = acc[1];
@@ -430,25 +511,30 @@ static void* worker(void* arg) {
     return NULL;
 }
 
-int oracle_render(const oracle_triangle* tris, int32_t n_tris, const oracle_material* mats, int32_t n_mats,
-                  const oracle_node* nodes, int32_t n_nodes, const oracle_uniforms* u, uint32_t frame_begin,
-                  uint32_t frame_count, const int32_t* rows, int32_t n_rows, int32_t mode, int32_t threads,
-                  float* out_accum, uint32_t* out_acc8, uint64_t* out_segments, uint64_t* out_tests) {
-    if (!tris || !mats || !u || !rows || n_rows < 0 || n_tris < 0) return -1;
+/* Renders an arbitrary list of pixels ((x, y) pairs); out_accum / out_acc8
+ * hold n_px * 4 entries in list order. */
+int oracle_render_pixels(const oracle_triangle* tris, int32_t n_tris, const oracle_material* mats, int32_t n_mats,
+                         const oracle_node* nodes, int32_t n_nodes, const oracle_uniforms* u, uint32_t frame_begin,
+                         uint32_t frame_count, const int32_t* px, int64_t n_px, int32_t mode, int32_t threads,
+                         float* out_accum, uint32_t* out_acc8, uint64_t* out_segments, uint64_t* out_tests) {
+    if (!tris || !mats || !u || (!px && n_px > 0) || n_px < 0 || n_tris < 0) return -1;
     if (mode == 1 && (!nodes || n_nodes < 1)) return -2;
-    if (u->numRaysPerPixel < 1) return -3;
+    if (!u->basicShading && u->numRaysPerPixel < 1) return -3;
     for (int i = 0; i < n_tris; i++)
         if (tris[i].materialIndex < 0 || tris[i].materialIndex >= n_mats) return -4;
+    for (int64_t i = 0; i < n_px; i++)
+        if (px[2 * i] < 0 || px[2 * i] >= (int32_t)u->width || px[2 * i + 1] < 0 || px[2 * i + 1] >= (int32_t)u->height)
+            return -5;
     ctx_t c = {tris, n_tris, mats, n_mats, nodes, n_nodes, u, mode};
     job_t j;
     j.c = &c;
-    j.rows = rows;
-    j.n_rows = n_rows;
+    j.px = px;
+    j.n_px = n_px;
     j.frame_begin = frame_begin;
     j.frame_count = frame_count;
     j.out_rgba = out_accum;
     j.out_acc8 = out_acc8;
-    atomic_init(&j.next_row, 0);
+    atomic_init(&j.next_unit, 0);
     atomic_init(&j.segs, 0);
     atomic_init(&j.tests, 0);
     if (threads < 1) threads = 1;
@@ -460,6 +546,26 @@ int oracle_render(const oracle_triangle* tris, int32_t n_tris, const oracle_mate
     if (out_segments) *out_segments = atomic_load(&j.segs);
     if (out_tests) *out_tests = atomic_load(&j.tests);
     return 0;
+}
+
+/* Whole rows: out_accum / out_acc8 are [n_rows][W][4]. */
+int oracle_render(const oracle_triangle* tris, int32_t n_tris, const oracle_material* mats, int32_t n_mats,
+                  const oracle_node* nodes, int32_t n_nodes, const oracle_uniforms* u, uint32_t frame_begin,
+                  uint32_t frame_count, const int32_t* rows, int32_t n_rows, int32_t mode, int32_t threads,
+                  float* out_accum, uint32_t* out_acc8, uint64_t* out_segments, uint64_t* out_tests) {
+    if (!u || !rows || n_rows < 0) return -1;
+    const int64_t W = (int64_t)u->width;
+    int32_t* px = (int32_t*)malloc(sizeof(int32_t) * 2 * (size_t)(W * n_rows + 1));
+    if (!px) return -6;
+    for (int64_t r = 0; r < n_rows; r++)
+        for (int64_t x = 0; x < W; x++) {
+            px[2 * (r * W + x)] = (int32_t)x;
+            px[2 * (r * W + x) + 1] = rows[r];
+        }
+    int rc = oracle_render_pixels(tris, n_tris, mats, n_mats, nodes, n_nodes, u, frame_begin, frame_count, px,
+                                  W * n_rows, mode, threads, out_accum, out_acc8, out_segments, out_tests);
+    free(px);
+    return rc;
 }
 
 /* Single-call helpers for known-answer tests. */

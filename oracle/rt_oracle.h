@@ -57,6 +57,13 @@ int oracle_render(const oracle_triangle* tris, int32_t n_tris, const oracle_mate
                   uint32_t frame_count, const int32_t* rows, int32_t n_rows, int32_t mode, int32_t threads,
                   float* out_accum, uint32_t* out_acc8, uint64_t* out_segments, uint64_t* out_tests);
 
+/* Same, over an arbitrary pixel list px = n_px (x, y) pairs; outputs are
+ * n_px*4 in list order (bounded CPU samples of large configs). */
+int oracle_render_pixels(const oracle_triangle* tris, int32_t n_tris, const oracle_material* mats, int32_t n_mats,
+                         const oracle_node* nodes, int32_t n_nodes, const oracle_uniforms* u, uint32_t frame_begin,
+                         uint32_t frame_count, const int32_t* px, int64_t n_px, int32_t mode, int32_t threads,
+                         float* out_accum, uint32_t* out_acc8, uint64_t* out_segments, uint64_t* out_tests);
+
 uint32_t oracle_pcg_next(uint32_t* state, float* out);
 int oracle_ray_triangle(const float o[3], const float d[3], const oracle_triangle* t, float* dst);
 void oracle_sky(const float d[3], float out[3]);

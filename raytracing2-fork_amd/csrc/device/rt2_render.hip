@@ -57,6 +57,10 @@ struct RenderParams {
     int tile_tris;  // TILED: triangles per LDS tile
     const rt2_node* nodes;  // BVH traversal
     int stack_slots;        // BVH: per-lane stack entries (tree depth + 2)
+    int basicShadow;        // traceBasic: basicShadingShadow
+    float light[3];         // traceBasic: basicShadingLightPosition.xyz
+    const float4* bvh_recs; // BVH v2: child-pair records (4 float4 each)
+    int bvh_root;           // BVH v2: stack entry of node 0
 };
 
 enum : int { ST_NEED_ITEM = 0, ST_NEW_FRAME = 1, ST_NEW_RAY = 2, ST_TRACE = 3, ST_DONE = 4 };
@@ -803,7 +807,7 @@ __device__ __forceinline__ float ray_bounds(const f3& o, const f3& d, bool sx, b
 template <int BLOCK>
 __device__ __forceinline__ void closest_bvh(const f3& o, const f3& d, const rt2_node* __restrict__ nodes,
                                             const float4* __restrict__ tri, int* stack, int stack_slots,
-                                            float& best, int& bi, uint32_t& tests) {
+                                            float& best, int& bi, uint32_t& tests, uint32_t& visits) {
     const bool sx = d.x < 1e-6f && d.x > -1e-6f;
     const bool sy = d.y < 1e-6f && d.y > -1e-6f;
     const bool sz = d.z < 1e-6f && d.z > -1e-6f;
@@ -824,6 +828,7 @@ __device__ __forceinline__ void closest_bvh(const f3& o, const f3& d, const rt2_
                 if (mt_pass(q, bestK)) mt_exact(q, i, best, bi, bestK);
             }
         } else {  // compute.glsl:441-456
+            visits++;
             const int ia = meta.z, ib = meta.z + 1;
             const float dA = ray_bounds(o, d, sx, sy, sz, nodes[ia].bmin, nodes[ia].bmax);
             const float dB = ray_bounds(o, d, sx, sy, sz, nodes[ib].bmin, nodes[ib].bmax);
@@ -845,7 +850,7 @@ __global__ __launch_bounds__(BLOCK) void render_bvh(RenderParams p) {
     extern __shared__ int bvh_stack[];
     Lane L;
     lane_init(L);
-    uint32_t tests = 0;
+    uint32_t tests = 0, visits = 0;
     for (;;) {
         advance(L, p);
         if (!__any(L.st == ST_TRACE)) break;
@@ -854,14 +859,373 @@ __global__ __launch_bounds__(BLOCK) void render_bvh(RenderParams p) {
             L.segs += 1;
             float best = 1e38f;
             int bi = -1;
-            closest_bvh<BLOCK>(L.o, L.d, p.nodes, p.tri, bvh_stack, p.stack_slots, best, bi, tests);
+            closest_bvh<BLOCK>(L.o, L.d, p.nodes, p.tri, bvh_stack, p.stack_slots, best, bi, tests, visits);
             shade(L, p, best, bi);
         }
     }
     flush_counters(L, p);
-    unsigned long long t = tests;
-    for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
-    if (lane_id() == 0) atomicAdd(p.seg_counter + 1, t);  // leaf triangle tests
+    unsigned long long t = tests, v = visits;
+    for (int off = 32; off > 0; off >>= 1) {
+        t += __shfl_xor(t, off);
+        v += __shfl_xor(v, off);
+    }
+    if (lane_id() == 0) {
+        atomicAdd(p.seg_counter + 1, t);  // leaf triangle tests
+        atomicAdd(p.seg_counter + 2, v);  // interior node visits (diagnostic)
+    }
+}
+
+// ---------------------------------------------------------------------------
+// BVH traversal, v2: the same visiting order as closest_bvh, restructured for
+// SIMT efficiency.
+//  * Child-pair records (host-built, bvh_records): one 64-B record per
+//    interior node holds both children's boxes and their stack entries, so a
+//    pop costs one 64-B load instead of a meta load followed by two box loads.
+//    A stack entry >= 0 is an interior record; < 0 is ~(start << 5 | count)
+//    for a leaf (count 31 = look the range up in the node array).
+//  * Exact slab divisions without the IEEE divide sequence: with y = RN(1/d)
+//    computed once per segment, q0 = RN(n*y), r = fma(-q0, d, n) (exact),
+//    q1 = RN(q0 + r*y), repeated once more, is RN(n/d) (Markstein) for
+//    2^-60 <= |n| <= 2^60 (or n = 0) and 1e-6 <= |d| <= 1; a wave with any
+//    numerator outside that range takes the IEEE division for the node
+//    (verified against IEEE division by tests/test_gpu_bvh.py's check).
+//  * While-while scheduling: lanes traverse independently; a lane whose
+//    segment is finished idles until at least `T` lanes of the wave are
+//    finished (or none traverses), then those lanes shade, start their next
+//    segment or next ray together.  A heavy-tailed ray no longer holds the
+//    whole wave at the segment boundary.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float div_mk(float n, float d, float y) {
+    float q = n * y;
+    float r = fmaf(-q, d, n);
+    q = fmaf(r, y, q);
+    r = fmaf(-q, d, n);
+    return fmaf(r, y, q);
+}
+__device__ __forceinline__ bool div_mk_ok(float n) {
+    const float a = fabsf(n);
+    return (a <= 0x1p60f && a >= 0x1p-60f) || a == 0.0f;
+}
+
+struct SlabRay {
+    f3 o, d, y;  // y = RN(1/d) on unskipped axes
+    bool sx, sy, sz;
+};
+
+// rayBoundsIntersect (compute.glsl:382-408) on box (b0, b1), exact.
+template <bool IEEE>
+__device__ __forceinline__ float slab(const SlabRay& R, float b0x, float b0y, float b0z, float b1x, float b1y,
+                                      float b1z) {
+    float tMin = -1e32f, tMax = 1e32f;
+#define RT2_SLAB_AXIS(S, B0, B1, O, D, Y)                                  \
+    if (!S) {                                                              \
+        float t0, t1;                                                      \
+        if constexpr (IEEE) {                                              \
+            t0 = (B0 - O) / D;                                             \
+            t1 = (B1 - O) / D;                                             \
+        } else {                                                           \
+            t0 = div_mk(B0 - O, D, Y);                                     \
+            t1 = div_mk(B1 - O, D, Y);                                     \
+        }                                                                  \
+        if (t0 > t1) { const float t_ = t0; t0 = t1; t1 = t_; }            \
+        if (tMin < t0) tMin = t0;                                          \
+        if (tMax > t1) tMax = t1;                                          \
+    }
+    RT2_SLAB_AXIS(R.sx, b0x, b1x, R.o.x, R.d.x, R.y.x)
+    RT2_SLAB_AXIS(R.sy, b0y, b1y, R.o.y, R.d.y, R.y.y)
+    RT2_SLAB_AXIS(R.sz, b0z, b1z, R.o.z, R.d.z, R.y.z)
+#undef RT2_SLAB_AXIS
+    return (tMin >= tMax || tMax < 0.0f) ? 1e38f : tMin;
+}
+
+__device__ __forceinline__ bool slab_numerators_ok(const SlabRay& R, const float4& r0, const float4& r1,
+                                                   const float4& r2) {
+    bool ok = true;
+    if (!R.sx) ok = ok && div_mk_ok(r0.x - R.o.x) && div_mk_ok(r0.w - R.o.x) && div_mk_ok(r1.z - R.o.x) &&
+                    div_mk_ok(r2.y - R.o.x);
+    if (!R.sy) ok = ok && div_mk_ok(r0.y - R.o.y) && div_mk_ok(r1.x - R.o.y) && div_mk_ok(r1.w - R.o.y) &&
+                    div_mk_ok(r2.z - R.o.y);
+    if (!R.sz) ok = ok && div_mk_ok(r0.z - R.o.z) && div_mk_ok(r1.y - R.o.z) && div_mk_ok(r2.x - R.o.z) &&
+                    div_mk_ok(r2.w - R.o.z);
+    return ok;
+}
+
+struct TravState {
+    int sp;  // > 0 traversing, 0 idle, -1 finished (awaiting shade)
+    float best, bestK;
+    int bi;
+    SlabRay R;
+};
+
+__device__ __forceinline__ void begin_segment(Lane& L, TravState& T, int* st, int root) {
+    L.bounce += 1;
+    L.segs += 1;
+    T.best = 1e38f;
+    T.bestK = 1e38f * 1.0009765625f;
+    T.bi = -1;
+    T.R.o = L.o;
+    T.R.d = L.d;
+    T.R.sx = L.d.x < 1e-6f && L.d.x > -1e-6f;
+    T.R.sy = L.d.y < 1e-6f && L.d.y > -1e-6f;
+    T.R.sz = L.d.z < 1e-6f && L.d.z > -1e-6f;
+    T.R.y = mk(T.R.sx ? 0.0f : 1.0f / L.d.x, T.R.sy ? 0.0f : 1.0f / L.d.y, T.R.sz ? 0.0f : 1.0f / L.d.z);
+    st[0] = root;
+    T.sp = 1;
+}
+
+// One pop of the lane's stack (compute.glsl:419-457).
+template <int BLOCK>
+__device__ __forceinline__ void bvh_step(TravState& T, int* st, const float4* __restrict__ recs,
+                                         const rt2_node* __restrict__ nodes, const float4* __restrict__ tri,
+                                         int stack_slots, uint32_t& tests, uint32_t& visits) {
+    T.sp -= 1;
+    const int e = st[T.sp * BLOCK];
+    if (e < 0) {  // leaf: compute.glsl:429-435
+        const int v = ~e;
+        int start = v >> 5, cnt = v & 31;
+        if (cnt == 31) {
+            const int4 meta = *reinterpret_cast<const int4*>(&nodes[start].triangleIndex);
+            start = meta.x;
+            cnt = max(meta.y, 0);
+        }
+        tests += (uint32_t)cnt;
+        for (int i = start; i < start + cnt; i++) {
+            const float4* t = tri + 3 * i;
+            const MtQ q = mt_quantities(T.R.o, T.R.d, t[0], t[1], t[2]);
+            if (mt_pass(q, T.bestK)) mt_exact(q, i, T.best, T.bi, T.bestK);
+        }
+    } else {  // compute.glsl:437-456
+        visits++;
+        const float4* rp = recs + 4 * e;
+        const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
+        const float4 r3 = rp[3];
+        float dA, dB;
+        if (__builtin_expect(__all(slab_numerators_ok(T.R, r0, r1, r2)), 1)) {
+            dA = slab<false>(T.R, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y);
+            dB = slab<false>(T.R, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w);
+        } else {
+            dA = slab<true>(T.R, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y);
+            dB = slab<true>(T.R, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w);
+        }
+        const int eA = __float_as_int(r3.x), eB = __float_as_int(r3.y);
+        const bool nearA = dA < dB;
+        const float dNear = nearA ? dA : dB;
+        const float dFar = nearA ? dB : dA;
+        const int iNear = nearA ? eA : eB;
+        const int iFar = nearA ? eB : eA;
+        if (dFar < T.best && T.sp < stack_slots) st[(T.sp++) * BLOCK] = iFar;
+        if (dNear < T.best && T.sp < stack_slots) st[(T.sp++) * BLOCK] = iNear;
+    }
+    if (T.sp == 0) T.sp = -1;
+}
+
+template <int BLOCK, int THRESH>
+__global__ __launch_bounds__(BLOCK) void render_bvh2(RenderParams p) {
+    extern __shared__ int bvh_stack[];
+    int* st = bvh_stack + threadIdx.x;
+    const float4* __restrict__ recs = p.bvh_recs;
+    Lane L;
+    lane_init(L);
+    TravState T;
+    T.sp = 0;
+    T.best = T.bestK = 1e38f;
+    T.bi = -1;
+    uint32_t tests = 0, visits = 0;
+    for (;;) {
+        // phase A: finished lanes shade; lanes between rays advance; new segments start
+        if (T.sp < 0) {
+            shade(L, p, T.best, T.bi);
+            T.sp = 0;
+        }
+        advance(L, p);
+        if (L.st == ST_TRACE && T.sp == 0) begin_segment(L, T, st, p.bvh_root);
+        if (!__any(T.sp > 0)) break;
+        // phase B: traverse until THRESH lanes have finished (or none traverses)
+        for (;;) {
+            if (T.sp > 0) bvh_step<BLOCK>(T, st, recs, p.nodes, p.tri, p.stack_slots, tests, visits);
+            const unsigned long long fin = __ballot(T.sp < 0);
+            if (!__any(T.sp > 0) || __popcll(fin) >= (unsigned)THRESH) break;
+        }
+    }
+    flush_counters(L, p);
+    unsigned long long t = tests, v = visits;
+    for (int off = 32; off > 0; off >>= 1) {
+        t += __shfl_xor(t, off);
+        v += __shfl_xor(v, off);
+    }
+    if (lane_id() == 0) {
+        atomicAdd(p.seg_counter + 1, t);  // leaf triangle tests
+        atomicAdd(p.seg_counter + 2, v);  // interior node visits (diagnostic)
+    }
+}
+
+// Division check for div_mk (test hook): n, d drawn from the ranges above.
+__global__ void div_check_kernel(uint32_t seed, unsigned long long count, unsigned long long* bad,
+                                 uint32_t* first) {
+    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+    unsigned long long nbad = 0;
+    for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) {
+        uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+        h ^= h >> 16;
+        h *= 0x7feb352du;
+        h ^= h >> 15;
+        h *= 0x846ca68bu;
+        h ^= h >> 16;
+        uint32_t g = h * 747796405u + 2891336453u;
+        g = ((g >> ((g >> 28u) + 4u)) ^ g) * 277803737u;
+        g ^= g >> 22;
+        // n: |n| in [2^-60, 2^60], random sign/mantissa; d: |d| in [2^-20, 1]
+        const uint32_t ne = 127 - 60 + (h % 121u);
+        const float n = __uint_as_float((h & 0x80000000u) | (ne << 23) | (g & 0x7fffffu));
+        const uint32_t de = 127 - 20 + ((g >> 23) % 21u);
+        float d = __uint_as_float(((g << 8) & 0x80000000u) | (de << 23) | ((h * 2246822519u) & 0x7fffffu));
+        if (fabsf(d) < 1e-6f) d = copysignf(1e-6f, d);
+        if (fabsf(d) > 1.0f) d = copysignf(1.0f, d);
+        const float y = 1.0f / d;
+        const float q = div_mk(n, d, y);
+        const float ref = n / d;
+        if (__float_as_uint(q) != __float_as_uint(ref)) {
+            nbad++;
+            atomicCAS(first, 0xffffffffu, (uint32_t)i);
+        }
+    }
+    if (nbad) atomicAdd(bad, nbad);
+}
+
+// ---------------------------------------------------------------------------
+// traceBasic preview (compute.glsl:565-645 + main's basicShading branch,
+// :672-678): one deterministic ray per pixel, no RNG, no tonemap.  One thread
+// per pixel; the closest hit is the brute-force masked sweep (triangles through
+// the scalar cache) or the BVH walk, whichever traversal the scene selects.
+// ---------------------------------------------------------------------------
+template <int BLOCK, bool BVH>
+__device__ __forceinline__ void closest_any(const RenderParams& p, const f3& o, const f3& d, int* stack, float& best,
+                                            int& bi, uint32_t& tests) {
+    best = 1e38f;
+    bi = -1;
+    if constexpr (BVH) {
+        uint32_t visits = 0;
+        closest_bvh<BLOCK>(o, d, p.nodes, p.tri, stack, p.stack_slots, best, bi, tests, visits);
+    } else {
+        float bestK = 1e38f * 1.0009765625f;
+        sweep_masked<8, true>(o, d, nullptr, (const float*)p.tri, p.n_tris, 0, best, bi, bestK);
+    }
+}
+
+template <int BLOCK, bool BVH>
+__device__ __forceinline__ f3 trace_basic(const RenderParams& p, f3 o, f3 d, int* stack, uint32_t& segs,
+                                          uint32_t& tests) {
+    f3 cum = mk(0.0f, 0.0f, 0.0f);
+    bool inside = false;  // `Ray ray;` leaves insideGlass undefined (:674); false here and in the oracle
+    int bc = 0;
+    while (bc < p.maxBounce) {
+        bc++;
+        segs++;
+        float best;
+        int bi;
+        closest_any<BLOCK, BVH>(p, o, d, stack, best, bi, tests);
+        if (bi < 0) {
+            cum = add(cum, sky(d));
+            break;
+        }
+        const float4 t2 = p.tri[3 * bi + 2];
+        const f3 normal = normalize(mk(t2.y, t2.z, t2.w));
+        const f3 hitPoint = add(o, muls(d, best));
+        o = sub(hitPoint, muls(normal, 1e-4f));  // :579
+        const rt2_material m = p.mats[p.tri_mtl[bi]];
+        switch (m.materialType) {
+        case RT2_SPECULAR:
+            cum = add(cum, xyz4(m.color));
+            d = reflect(d, normal);
+            break;
+        case RT2_DIFFUSE:
+        case RT2_TEXTURE:
+        case RT2_CHECKER: {
+            f3 color;
+            if (m.materialType == RT2_TEXTURE) {
+                color = mk(0.0f, 0.0f, 0.0f);  // no textures bound: black, as in trace()
+            } else if (m.materialType == RT2_DIFFUSE) {
+                color = xyz4(m.color);
+            } else {
+                const float s = m.checkerScale;
+                bool black = false;
+                if (s > 0.0f) {
+                    const float sum = floorf(o.x * s) + floorf(o.y * s) + floorf(o.z * s);
+                    black = sum - 2.0f * floorf(sum / 2.0f) == 0.0f;
+                }
+                color = black ? mk(0.0f, 0.0f, 0.0f) : mk(1.0f, 1.0f, 1.0f);
+            }
+            cum = add(cum, color);
+            if (p.basicShadow) {  // :614-621, shadow ray toward the preview light
+                const f3 toLight = normalize(sub(ld3(p.light), hitPoint));
+                segs++;
+                float b2;
+                int bi2;
+                closest_any<BLOCK, BVH>(p, o, toLight, stack, b2, bi2, tests);
+                return divs(bi2 >= 0 ? divs(cum, 5.0f) : cum, (float)bc);
+            }
+            return divs(cum, (float)bc);
+        }
+        case RT2_LIGHT: {  // normalizeColor, :462-470
+            const f3 e = xyz4(m.emissionColor);
+            const float mx = fmaxf(fmaxf(e.x, e.y), e.z);
+            return mx > 1.0f ? divs(e, mx) : e;
+        }
+        case RT2_GLASS: {
+            const float eta = inside ? m.refractiveIndex : 1.0f / m.refractiveIndex;
+            bool refr;
+            d = refract_(d, normal, eta, refr);
+            inside = refr != inside;
+            cum = xyz4(m.color);
+            break;
+        }
+        case RT2_GLASS_HIGHLIGHT:  // `if (bounceCount == 0)` never holds after bounceCount++
+            break;
+        default:
+            return mk(1.0f, 0.0f, 1.0f);
+        }
+    }
+    return divs(cum, (float)bc);
+}
+
+template <int BLOCK, bool BVH>
+__global__ __launch_bounds__(BLOCK) void render_basic(RenderParams p) {
+    extern __shared__ int basic_stack[];
+    uint32_t segs = 0, tests = 0;
+    const unsigned long long it = (unsigned long long)blockIdx.x * BLOCK + threadIdx.x;
+    if (it < p.n_items) {
+        const uint32_t item = (uint32_t)it;
+        const int lr = (int)(item / (uint32_t)p.W);
+        const int x = (int)(item - (uint32_t)lr * (uint32_t)p.W);
+        const int y = shard_row(lr, p.tile_rows, p.rank, p.nranks);
+        const float px = (float)(x * 2 - p.W) / (float)p.W;
+        const float py = (float)(y * 2 - p.H) / (float)p.H;
+        const f3 dir = normalize(add(add(ld3(p.vpFront), muls(ld3(p.vpRight), px)), muls(ld3(p.vpUp), py)));
+        // frame-independent: traced once, accumulated frame_count times in order
+        const f3 c = trace_basic<BLOCK, BVH>(p, ld3(p.cam), dir, basic_stack, segs, tests);
+        float4 a = p.accum[item];
+        for (uint32_t f = 0; f < p.frame_count; f++) a = make_float4(a.x + c.x, a.y + c.y, a.z + c.z, 0.0f);
+        p.accum[item] = a;
+        if (p.accum8) {
+            const uint32_t qx = (uint32_t)(clampf(c.x, 0.0f, 1.0f) * 255.0f + 0.5f);
+            const uint32_t qy = (uint32_t)(clampf(c.y, 0.0f, 1.0f) * 255.0f + 0.5f);
+            const uint32_t qz = (uint32_t)(clampf(c.z, 0.0f, 1.0f) * 255.0f + 0.5f);
+            const uint4 q = p.accum8[item];
+            p.accum8[item] = make_uint4(q.x + qx * p.frame_count, q.y + qy * p.frame_count,
+                                        q.z + qz * p.frame_count, 0u);
+        }
+    }
+    // counters as the reference would do the work: once per frame
+    unsigned long long s = (unsigned long long)segs * p.frame_count;
+    unsigned long long t = (unsigned long long)tests * p.frame_count;
+    for (int off = 32; off > 0; off >>= 1) {
+        s += __shfl_xor(s, off);
+        t += __shfl_xor(t, off);
+    }
+    if (lane_id() == 0) {
+        atomicAdd(p.seg_counter, s);
+        if (BVH) atomicAdd(p.seg_counter + 1, t);
+    }
 }
 
 // Pre-transform: RTXTriangle (80 B) -> {a, e0, e1, n} (48 B) + material index.
@@ -952,6 +1316,8 @@ struct rt2_scene {
     int* d_mtl = nullptr;
     rt2_material* d_mats = nullptr;
     rt2_node* d_nodes = nullptr;
+    float4* d_recs = nullptr;                   // BVH v2 child-pair records
+    int bvh_root = 0;                           // BVH v2 stack entry of node 0
     unsigned long long* d_counters = nullptr;  // [0] item counter, [1] segments
     unsigned long long samples = 0, tests_per_seg = 0;
     int variant = 0;
@@ -1004,6 +1370,49 @@ static int bvh_depth_check(const rt2_node* nodes, int n_nodes, int n_tris, std::
         }
     }
     return maxd;
+}
+
+// Child-pair records for render_bvh2 (layout: see bvh_step).  Interior nodes
+// are numbered in depth-first pre-order (parents before children, left
+// subtree first) so records of a subtree are contiguous.
+static int bvh_records(const rt2_node* nodes, int n_nodes, std::vector<float4>& rec, int& root, std::string& err) {
+    if (n_nodes >= (1 << 26)) {
+        err = "more than 2^26 nodes";
+        return -1;
+    }
+    std::vector<int> rid(n_nodes, -1);
+    int n_int = 0;
+    std::vector<int> stack{0};
+    while (!stack.empty()) {
+        const int i = stack.back();
+        stack.pop_back();
+        if (nodes[i].childIndex == -1) continue;
+        rid[i] = n_int++;
+        stack.push_back(nodes[i].childIndex + 1);
+        stack.push_back(nodes[i].childIndex);
+    }
+    auto enc = [&](int i) -> int {
+        const rt2_node& n = nodes[i];
+        if (n.childIndex != -1) return rid[i];
+        const int cnt = std::max(n.triangleCount, 0);
+        const int start = cnt > 0 ? n.triangleIndex : 0;
+        if (cnt <= 30 && start >= 0 && start < (1 << 26)) return ~((start << 5) | cnt);
+        return ~((i << 5) | 31);
+    };
+    rec.assign((size_t)std::max(n_int, 1) * 4, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+    for (int i = 0; i < n_nodes; i++) {
+        if (rid[i] < 0) continue;
+        const rt2_node& A = nodes[nodes[i].childIndex];
+        const rt2_node& B = nodes[nodes[i].childIndex + 1];
+        float4* r = &rec[(size_t)rid[i] * 4];
+        r[0] = make_float4(A.bmin[0], A.bmin[1], A.bmin[2], A.bmax[0]);
+        r[1] = make_float4(A.bmax[1], A.bmax[2], B.bmin[0], B.bmin[1]);
+        r[2] = make_float4(B.bmin[2], B.bmax[0], B.bmax[1], B.bmax[2]);
+        int e[4] = {enc(nodes[i].childIndex), enc(nodes[i].childIndex + 1), 0, 0};
+        std::memcpy(&r[3], e, sizeof(e));
+    }
+    root = enc(0);
+    return n_int;
 }
 
 extern "C" int rt2_scene_set_traversal(rt2_scene* s, int traversal) {
@@ -1068,6 +1477,14 @@ extern "C" int rt2_scene_create(const rt2_triangle* tris, int32_t n_tris, const 
         }
         HIPCHECK(hipMalloc(&s->d_nodes, (size_t)n_nodes * sizeof(rt2_node)));
         HIPCHECK(hipMemcpy(s->d_nodes, nodes, (size_t)n_nodes * sizeof(rt2_node), hipMemcpyHostToDevice));
+        std::vector<float4> rec;
+        if (bvh_records(nodes, n_nodes, rec, s->bvh_root, err) < 0) {
+            rt2h::set_error("rt2_scene_create: bad node array: " + err);
+            delete s;
+            return -1;
+        }
+        HIPCHECK(hipMalloc(&s->d_recs, rec.size() * sizeof(float4)));
+        HIPCHECK(hipMemcpy(s->d_recs, rec.data(), rec.size() * sizeof(float4), hipMemcpyHostToDevice));
     }
     if (n_tris > 0) {
         hipLaunchKernelGGL(prep_triangles, dim3((n_tris + 255) / 256), dim3(256), 0, 0, s->d_raw, n_tris, s->d_tri,
@@ -1087,6 +1504,7 @@ extern "C" void rt2_scene_destroy(rt2_scene* s) {
     (void)hipFree(s->d_mtl);
     (void)hipFree(s->d_mats);
     (void)hipFree(s->d_nodes);
+    (void)hipFree(s->d_recs);
     (void)hipFree(s->d_counters);
     delete s;
 }
@@ -1114,7 +1532,7 @@ namespace {
 constexpr int kTileTris = 1024;  // 48 KiB of LDS per tile
 
 // Kernel variants (rt2_scene_set_variant); 0 = auto = the default below.
-enum Kind : int { K_RESIDENT = 0, K_TILED = 1, K_SMEM = 2, K_BVH = 3 };
+enum Kind : int { K_RESIDENT = 0, K_TILED = 1, K_SMEM = 2, K_BVH = 3, K_BVH2 = 4 };
 struct Variant {
     int kind;
     int block;
@@ -1131,6 +1549,8 @@ hipError_t launch_t(const RenderParams& p, int blocks, size_t lds, hipStream_t s
         hipLaunchKernelGGL((render_smem<BLOCK, MT % 1000, MT / 1000>), dim3(blocks), dim3(BLOCK), 0, st, p);
     else if constexpr (KIND == K_BVH)
         hipLaunchKernelGGL((render_bvh<BLOCK>), dim3(blocks), dim3(BLOCK), lds, st, p);
+    else if constexpr (KIND == K_BVH2)
+        hipLaunchKernelGGL((render_bvh2<BLOCK, MT>), dim3(blocks), dim3(BLOCK), lds, st, p);
     else
         hipLaunchKernelGGL((render_resident<BLOCK, MT, UNROLL>), dim3(blocks), dim3(BLOCK), lds, st, p);
     return hipGetLastError();
@@ -1143,6 +1563,8 @@ hipError_t occ_t(int* occ, size_t lds) {
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_smem<BLOCK, MT % 1000, MT / 1000>, BLOCK, 0);
     else if constexpr (KIND == K_BVH)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_bvh<BLOCK>, BLOCK, lds);
+    else if constexpr (KIND == K_BVH2)
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_bvh2<BLOCK, MT>, BLOCK, lds);
     else
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_resident<BLOCK, MT, UNROLL>, BLOCK, lds);
 }
@@ -1189,11 +1611,17 @@ const Variant kVariants[] = {
     RT2_VARIANT(K_BVH, 256, 0, 1, "bvh/256"),                        // 37: default (BVH traversal)
     RT2_VARIANT(K_BVH, 128, 0, 1, "bvh/128"),                        // 38
     RT2_VARIANT(K_BVH, 512, 0, 1, "bvh/512"),                        // 39
+    RT2_VARIANT(K_BVH2, 256, 16, 1, "bvh2/256/t16"),                 // 40
+    RT2_VARIANT(K_BVH2, 256, 8, 1, "bvh2/256/t8"),                   // 41
+    RT2_VARIANT(K_BVH2, 256, 32, 1, "bvh2/256/t32"),                 // 42
+    RT2_VARIANT(K_BVH2, 128, 16, 1, "bvh2/128/t16"),                 // 43
+    RT2_VARIANT(K_BVH2, 64, 16, 1, "bvh2/64/t16"),                   // 44
+    RT2_VARIANT(K_BVH2, 256, 1, 1, "bvh2/256/t1"),                   // 45
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr size_t kResidentMaxBytes = 112 * 1024;
 constexpr int kSmemMaxTris = 16384;
-constexpr int kDefaultBvhVariant = 37;
+constexpr int kDefaultBvhVariant = 40;
 }  // namespace
 
 extern "C" const char* rt2_variant_name(int v) { return v >= 0 && v < kNumVariants ? kVariants[v].name : nullptr; }
@@ -1204,11 +1632,7 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
         rt2h::set_error("rt2_render: null argument");
         return -1;
     }
-    if (u->basicShading) {
-        rt2h::set_error("rt2_render: basicShading (traceBasic preview) is not on this path");
-        return -1;
-    }
-    if (u->numRaysPerPixel < 1 || u->width < 1 || u->height < 1) {
+    if ((!u->basicShading && u->numRaysPerPixel < 1) || u->width < 1 || u->height < 1) {
         rt2h::set_error("rt2_render: numRaysPerPixel, width and height must be >= 1");
         return -1;
     }
@@ -1265,28 +1689,53 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     HIPCHECK(hipMemsetAsync(s->d_counters, 0, sizeof(unsigned long long), st));
     HIPCHECK(hipMemsetAsync(s->d_counters + 6, 0xff, sizeof(unsigned long long), st));  // diag: min wave end
     HIPCHECK(hipMemsetAsync(s->d_counters + 7, 0, sizeof(unsigned long long), st));     // diag: max wave end
+    p.nodes = s->d_nodes;
+    p.stack_slots = s->bvh_depth + 2;
+    if (u->basicShading) {  // traceBasic preview: one thread per pixel
+        p.basicShadow = u->basicShadingShadow;
+        cp(p.light, u->basicShadingLightPosition);
+        constexpr int kBasicBlock = 256;
+        const unsigned long long blocks = (p.n_items + kBasicBlock - 1) / kBasicBlock;
+        if (s->traversal == RT2_TRAVERSAL_BVH) {
+            const size_t lds = (size_t)p.stack_slots * kBasicBlock * sizeof(int);
+            hipLaunchKernelGGL((render_basic<kBasicBlock, true>), dim3((unsigned)blocks), dim3(kBasicBlock), lds, st,
+                               p);
+            s->last_kind = K_BVH;
+        } else {
+            hipLaunchKernelGGL((render_basic<kBasicBlock, false>), dim3((unsigned)blocks), dim3(kBasicBlock), 0, st,
+                               p);
+            s->last_kind = K_SMEM;
+        }
+        HIPCHECK(hipGetLastError());
+        s->last_variant = -1;
+        s->samples += p.n_items * (unsigned long long)frame_count;
+        s->tests_per_seg = (unsigned long long)s->n_tris;
+        return 0;
+    }
     const size_t resident_bytes = (size_t)3 * sizeof(float4) * (size_t)std::max(s->n_tris, 1);
     const bool fits = resident_bytes <= kResidentMaxBytes;
     int vi = s->variant;
     // auto: scalar-path kernel for small scenes (config B: 1,208 triangles),
     // LDS-tiled sweep for large ones (config C/E: 100k-1M triangles)
     if (s->traversal == RT2_TRAVERSAL_BVH) {
-        if (vi <= 0 || vi >= kNumVariants || kVariants[vi].kind != K_BVH) vi = kDefaultBvhVariant;
+        if (vi <= 0 || vi >= kNumVariants || (kVariants[vi].kind != K_BVH && kVariants[vi].kind != K_BVH2))
+            vi = kDefaultBvhVariant;
     } else {
-        if (vi <= 0 || vi >= kNumVariants || kVariants[vi].kind == K_BVH) vi = s->n_tris <= kSmemMaxTris ? 0 : 2;
+        if (vi <= 0 || vi >= kNumVariants || kVariants[vi].kind == K_BVH || kVariants[vi].kind == K_BVH2)
+            vi = s->n_tris <= kSmemMaxTris ? 0 : 2;
         if (kVariants[vi].kind == K_RESIDENT && !fits) vi = 2;  // a resident variant cannot hold this scene
     }
     const Variant& V = kVariants[vi];
-    p.nodes = s->d_nodes;
-    p.stack_slots = s->bvh_depth + 2;
     size_t lds = 0;
     if (V.kind == K_TILED)
         lds = (size_t)3 * sizeof(float4) * kTileTris;
     else if (V.kind == K_RESIDENT)
         lds = resident_bytes;
-    else if (V.kind == K_BVH)
+    else if (V.kind == K_BVH || V.kind == K_BVH2)
         lds = (size_t)p.stack_slots * V.block * sizeof(int);
-    s->last_kind = V.kind;
+    p.bvh_recs = s->d_recs;
+    p.bvh_root = s->bvh_root;
+    s->last_kind = V.kind == K_BVH2 ? K_BVH : V.kind;
     int occ = 0;
     HIPCHECK(V.occupancy(&occ, lds));
     occ = std::max(occ, 1);
@@ -1425,6 +1874,23 @@ extern "C" int rt2_device_rcp_check(uint32_t lo, uint32_t hi, int variant, unsig
     HIPCHECK(hipMemcpy((char*)d + 8, &init, 4, hipMemcpyHostToDevice));
     const unsigned long long count = (unsigned long long)hi - lo + 1;
     hipLaunchKernelGGL(rcp_check_kernel, dim3(4096), dim3(256), 0, 0, lo, count, variant, d, (uint32_t*)((char*)d + 8));
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipMemcpy(mismatches, d, 8, hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(first_bad, (char*)d + 8, 4, hipMemcpyDeviceToHost));
+    (void)hipFree(d);
+    return 0;
+}
+
+// Not in rt2.h (test hook): div_mk against IEEE division on `count` random
+// (n, d) pairs of the ranges bvh_step uses it on.
+extern "C" int rt2_device_div_check(uint32_t seed, unsigned long long count, unsigned long long* mismatches,
+                                    uint32_t* first_bad) {
+    unsigned long long* d = nullptr;
+    HIPCHECK(hipMalloc(&d, 16));
+    HIPCHECK(hipMemset(d, 0, 8));
+    uint32_t init = 0xffffffffu;
+    HIPCHECK(hipMemcpy((char*)d + 8, &init, 4, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(div_check_kernel, dim3(8192), dim3(256), 0, 0, seed, count, d, (uint32_t*)((char*)d + 8));
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipMemcpy(mismatches, d, 8, hipMemcpyDeviceToHost));
     HIPCHECK(hipMemcpy(first_bad, (char*)d + 8, 4, hipMemcpyDeviceToHost));

@@ -227,6 +227,7 @@ def lib() -> C.CDLL:
         "rt2_write_png": (C.c_int, [C.c_char_p, I32, I32, I32, P, I32]),
         "rt2_device_selftest": (C.c_int, [P, I32, P]),
         "rt2_device_rcp_check": (C.c_int, [U32, U32, C.c_int, C.POINTER(C.c_ulonglong), C.POINTER(U32)]),
+        "rt2_device_div_check": (C.c_int, [U32, C.c_ulonglong, C.POINTER(C.c_ulonglong), C.POINTER(U32)]),
         "rt2_variant_name": (C.c_char_p, [C.c_int]),
         "rt2_scene_diag": (C.c_int, [P, C.POINTER(C.c_ulonglong), C.POINTER(C.c_int)]),
     }

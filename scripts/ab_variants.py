@@ -21,11 +21,15 @@ ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--width", type=int, default=0)
 ap.add_argument("--height", type=int, default=0)
 ap.add_argument("--rays", type=int, default=0)
+ap.add_argument("--frames", type=int, default=0)
+ap.add_argument("--traversal", default="brute", choices=["brute", "bvh"])
 a = ap.parse_args()
 sd, spec = rt2.build_config_scene(a.config)
 W, H, R = a.width or spec.width, a.height or spec.height, a.rays or spec.rays
 u = rt2.offline_uniforms(W, H, spec.bounces, R, sd.num_triangles)
 scene = rt2.Scene(sd, 0)
+scene.set_traversal(a.traversal)
+F = a.frames or spec.frames
 variants = [int(v) for v in a.variants.split(",")]
 times = {v: [] for v in variants}
 ref = None
@@ -37,13 +41,16 @@ for rnd in range(a.rounds):
         torch.cuda.synchronize()
         scene.stats(reset=True)
         t = time.perf_counter()
-        img = scene.render_host(u, 0, spec.frames)
+        img = scene.render_host(u, 0, F)
         times[v].append(time.perf_counter() - t)
         scene.stats(reset=True)
         c = (C.c_ulonglong * 8)()
         lv = C.c_int()
         rt2.lib().rt2_scene_diag(scene._p, c, C.byref(lv))
-        if c[2]:
+        if a.traversal == "bvh":
+            diag[v] = dict(segments=c[1], tests_per_segment=c[2] / max(c[1], 1),
+                           interior_visits_per_segment=c[3] / max(c[1], 1))
+        elif c[2]:
             diag[v] = dict(segments=c[1], groups=c[2], groups_with_survivor=c[3], exact_iters=c[4],
                            lane_survivors=c[5], frac_groups_exact=c[3] / c[2], exact_iters_per_group=c[4] / c[2],
                            lane_survivor_rate=c[5] / (c[2] * 64 * 4),
@@ -53,7 +60,7 @@ for rnd in range(a.rounds):
                 ref = img
             assert np.array_equal(img, ref), f"variant {v} differs"
 st = scene.stats(reset=True)
-samples = W * H * R * spec.frames
+samples = W * H * R * F
 out = {}
 for v in variants:
     med = float(np.median(times[v]))

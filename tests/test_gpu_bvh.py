@@ -88,3 +88,85 @@ def test_bvh_requires_nodes_and_validates(rt2mod, torch_cuda):
     nodes["childIndex"][0] = 99
     with pytest.raises(rt2mod.RT2Error, match="out of range"):
         rt2mod.Scene(triangles=sd.triangles(), materials=sd.materials(), nodes=nodes)
+
+
+BVH2_VARIANTS = [40, 41, 42, 43, 44, 45]  # render_bvh2: child-pair records, Markstein slabs, while-while
+
+
+def test_markstein_slab_division(rt2mod, torch_cuda):
+    """div_mk == IEEE n/d on 2^32 random pairs of the ranges bvh_step uses it on."""
+    import ctypes as C
+    bad = C.c_ulonglong(0)
+    first = C.c_uint32(0)
+    for seed in (1, 2, 3, 4):
+        assert rt2mod.lib().rt2_device_div_check(seed, 1 << 30, C.byref(bad), C.byref(first)) == 0
+        assert bad.value == 0, f"seed {seed}: {bad.value} mismatches, first index {first.value}"
+
+
+@pytest.mark.parametrize("variant", BVH2_VARIANTS)
+def test_bvh2_matches_oracle_bvh(rt2mod, oraclemod, config_scene, torch_cuda, variant):
+    sd, spec = config_scene("B")
+    W, H, R = 192, 108, 8
+    u = rt2mod.offline_uniforms(W, H, spec.bounces, R, sd.num_triangles)
+    scene = bvh_scene(rt2mod, sd)
+    scene.set_variant(variant)
+    img = scene.render_host(u, 0, 2)
+    st = scene.stats(reset=True)
+    acc, _, segs, tests = oraclemod.render(sd.triangles(), sd.materials(), u, np.arange(H), 0, 2, "bvh",
+                                           nodes=sd.nodes())
+    assert_exact(img, acc[..., :3] / np.float32(2), f"bvh2 variant {variant}")
+    assert st.segments == segs
+    assert st.tests == tests
+
+
+def test_bvh2_large_mesh_and_diverse(rt2mod, oraclemod, config_scene, torch_cuda):
+    sd, spec = config_scene("C")
+    u = rt2mod.offline_uniforms(96, 54, spec.bounces, 4, sd.num_triangles)
+    scene = bvh_scene(rt2mod, sd)
+    scene.set_variant(40)
+    img = scene.render_host(u, 0, 1)
+    ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(54), 0, 1, "bvh")
+    assert_exact(img, ref, "bvh2 config C")
+    M = rt2mod.Material
+    sd = rt2mod.SceneData()
+    ids = [sd.add_material(m) for m in (M.diffuse((1, 0, 0)), M.diffuse((0, 1, 0)), M.diffuse((1, 1, 1)),
+                                        M.light((1, 1, 1), 15.0), M.glass((0.9, 0.95, 1.0), 1.5),
+                                        M.specular((1, 1, 1), (1, 1, 1), 1.0, 1.0), M.checker(8.0),
+                                        M.specular((0.8, 0.6, 0.3), (1, 1, 1), 0.7, 0.4))]
+    sd.create_diverse_cornell_box(10.0, *ids)
+    sd.build_bvh()
+    u = rt2mod.offline_uniforms(80, 60, 12, 3, sd.num_triangles)
+    scene = bvh_scene(rt2mod, sd)
+    scene.set_variant(40)
+    img = scene.render_host(u, 0, 2)
+    ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(60), 0, 2, "bvh")
+    assert_exact(img, ref, "bvh2 diverse")
+
+
+def test_bvh2_big_leaves_and_single_node(rt2mod, oraclemod, torch_cuda):
+    """Leaves of > 30 triangles take the node-array lookup; a one-node BVH is a leaf root."""
+    M = rt2mod.Material
+    rng = np.random.default_rng(5)
+    for n_tris in (1, 40, 300):
+        sd = rt2mod.SceneData()
+        sd.add_material(M.diffuse((0.8, 0.8, 0.8)))
+        sd.add_material(M.light((1, 1, 1), 5.0))
+        a = rng.uniform(-3, 3, (n_tris, 3)).astype(np.float32) + np.float32([0, 5, -5])
+        for i in range(n_tris):
+            sd.add_triangle(tuple(a[i]), tuple(a[i] + rng.uniform(-1, 1, 3)), tuple(a[i] + rng.uniform(-1, 1, 3)),
+                            i % 2)
+        sd.build_bvh()
+        nodes = sd.nodes().copy()
+        # one flat leaf over everything: exercises the count-31 escape and a leaf root
+        flat = nodes[:1].copy()
+        flat["childIndex"][0] = -1
+        flat["triangleIndex"][0] = 0
+        flat["triangleCount"][0] = n_tris
+        for nd in (nodes, flat):
+            scene = rt2mod.Scene(triangles=sd.triangles(), materials=sd.materials(), nodes=nd)
+            scene.set_traversal("bvh")
+            scene.set_variant(40)
+            u = rt2mod.offline_uniforms(48, 32, 6, 2, n_tris)
+            img = scene.render_host(u, 0, 1)
+            acc, _, _, _ = oraclemod.render(sd.triangles(), sd.materials(), u, np.arange(32), 0, 1, "bvh", nodes=nd)
+            assert_exact(img, acc[..., :3], f"bvh2 n={n_tris} nodes={len(nd)}")
