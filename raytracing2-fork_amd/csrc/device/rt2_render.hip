@@ -61,6 +61,7 @@ struct RenderParams {
     float light[3];         // traceBasic: basicShadingLightPosition.xyz
     const float4* bvh_recs; // BVH v2: child-pair records (4 float4 each)
     int bvh_root;           // BVH v2: stack entry of node 0
+    int recs_ok;            // BVH v3: every record coordinate in {0} U [2^-37, 2^59]
 };
 
 enum : int { ST_NEED_ITEM = 0, ST_NEW_FRAME = 1, ST_NEW_RAY = 2, ST_TRACE = 3, ST_DONE = 4 };
@@ -1059,6 +1060,167 @@ __global__ __launch_bounds__(BLOCK) void render_bvh2(RenderParams p) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// BVH traversal, v3 (render_bvh3): v2 plus
+//  * a wave-uniform fast path: when every lane's segment has no skipped axis
+//    (|d_i| >= 1e-6) and satisfies the Markstein preconditions by
+//    construction — origin components and (host-checked, p.recs_ok) box
+//    coordinates in {0} U [2^-37, 2^59], so every numerator b - o is 0 or in
+//    [2^-60, 2^60], and |d_i| <= 2 — the slab test runs branch-free with no
+//    per-numerator checks; otherwise the node takes the IEEE slab<true>;
+//  * one interior pop AND one leaf pop per lane per iteration (the leaf
+//    sub-step sees the near child just pushed), so the leaf body runs for
+//    more lanes at once.  The per-lane pop order is unchanged.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool mk_coord_ok(float c) {
+    const float a = fabsf(c);
+    return a == 0.0f || (a >= 0x1p-37f && a <= 0x1p59f);
+}
+
+struct TravState3 {
+    int sp;  // > 0 traversing, 0 idle, -1 finished (awaiting shade)
+    float best, bestK;
+    int bi;
+    bool fast;  // no skipped axis, Markstein preconditions hold
+    SlabRay R;
+};
+
+__device__ __forceinline__ void begin_segment3(Lane& L, TravState3& T, int* st, int root) {
+    L.bounce += 1;
+    L.segs += 1;
+    T.best = 1e38f;
+    T.bestK = 1e38f * 1.0009765625f;
+    T.bi = -1;
+    T.R.o = L.o;
+    T.R.d = L.d;
+    T.R.sx = L.d.x < 1e-6f && L.d.x > -1e-6f;
+    T.R.sy = L.d.y < 1e-6f && L.d.y > -1e-6f;
+    T.R.sz = L.d.z < 1e-6f && L.d.z > -1e-6f;
+    T.R.y = mk(T.R.sx ? 0.0f : 1.0f / L.d.x, T.R.sy ? 0.0f : 1.0f / L.d.y, T.R.sz ? 0.0f : 1.0f / L.d.z);
+    T.fast = !(T.R.sx || T.R.sy || T.R.sz) && mk_coord_ok(L.o.x) && mk_coord_ok(L.o.y) && mk_coord_ok(L.o.z) &&
+             fabsf(L.d.x) <= 2.0f && fabsf(L.d.y) <= 2.0f && fabsf(L.d.z) <= 2.0f;
+    st[0] = root;
+    T.sp = 1;
+}
+
+// Branch-free exact slab for the fast path (all axes live, div_mk valid).
+__device__ __forceinline__ float slab_fast(const SlabRay& R, float b0x, float b0y, float b0z, float b1x, float b1y,
+                                           float b1z) {
+    float tMin = -1e32f, tMax = 1e32f;
+#define RT2_SLAB_FAST(B0, B1, O, D, Y)                          \
+    {                                                           \
+        float t0 = div_mk(B0 - O, D, Y);                        \
+        float t1 = div_mk(B1 - O, D, Y);                        \
+        if (t0 > t1) { const float t_ = t0; t0 = t1; t1 = t_; } \
+        if (tMin < t0) tMin = t0;                               \
+        if (tMax > t1) tMax = t1;                               \
+    }
+    RT2_SLAB_FAST(b0x, b1x, R.o.x, R.d.x, R.y.x)
+    RT2_SLAB_FAST(b0y, b1y, R.o.y, R.d.y, R.y.y)
+    RT2_SLAB_FAST(b0z, b1z, R.o.z, R.d.z, R.y.z)
+#undef RT2_SLAB_FAST
+    return (tMin >= tMax || tMax < 0.0f) ? 1e38f : tMin;
+}
+
+template <int BLOCK>
+__device__ __forceinline__ void bvh_interior3(TravState3& T, int* st, int e, const float4* __restrict__ recs,
+                                              bool fast, int stack_slots, uint32_t& visits) {
+    visits++;
+    const float4* rp = recs + 4 * e;
+    const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
+    const float4 r3 = rp[3];
+    float dA, dB;
+    if (fast) {
+        dA = slab_fast(T.R, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y);
+        dB = slab_fast(T.R, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w);
+    } else {
+        dA = slab<true>(T.R, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y);
+        dB = slab<true>(T.R, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w);
+    }
+    const int eA = __float_as_int(r3.x), eB = __float_as_int(r3.y);
+    const bool nearA = dA < dB;
+    const float dNear = nearA ? dA : dB;
+    const float dFar = nearA ? dB : dA;
+    const int iNear = nearA ? eA : eB;
+    const int iFar = nearA ? eB : eA;
+    if (dFar < T.best && T.sp < stack_slots) st[(T.sp++) * BLOCK] = iFar;
+    if (dNear < T.best && T.sp < stack_slots) st[(T.sp++) * BLOCK] = iNear;
+}
+
+__device__ __forceinline__ void bvh_leaf3(TravState3& T, int e, const rt2_node* __restrict__ nodes,
+                                          const float4* __restrict__ tri, uint32_t& tests) {
+    const int v = ~e;
+    int start = v >> 5, cnt = v & 31;
+    if (cnt == 31) {
+        const int4 meta = *reinterpret_cast<const int4*>(&nodes[start].triangleIndex);
+        start = meta.x;
+        cnt = max(meta.y, 0);
+    }
+    tests += (uint32_t)cnt;
+    for (int i = start; i < start + cnt; i++) {
+        const float4* t = tri + 3 * i;
+        const MtQ q = mt_quantities(T.R.o, T.R.d, t[0], t[1], t[2]);
+        if (mt_pass(q, T.bestK)) mt_exact(q, i, T.best, T.bi, T.bestK);
+    }
+}
+
+template <int BLOCK, int THRESH>
+__global__ __launch_bounds__(BLOCK) void render_bvh3(RenderParams p) {
+    extern __shared__ int bvh_stack[];
+    int* st = bvh_stack + threadIdx.x;
+    const float4* __restrict__ recs = p.bvh_recs;
+    Lane L;
+    lane_init(L);
+    TravState3 T;
+    T.sp = 0;
+    T.best = T.bestK = 1e38f;
+    T.bi = -1;
+    T.fast = true;
+    uint32_t tests = 0, visits = 0;
+    for (;;) {
+        if (T.sp < 0) {
+            shade(L, p, T.best, T.bi);
+            T.sp = 0;
+        }
+        advance(L, p);
+        if (L.st == ST_TRACE && T.sp == 0) begin_segment3(L, T, st, p.bvh_root);
+        if (!__any(T.sp > 0)) break;
+        const bool fast = p.recs_ok && __all(T.fast || T.sp <= 0);
+        for (;;) {
+            // interior sub-step
+            if (T.sp > 0) {
+                const int e = st[(T.sp - 1) * BLOCK];
+                if (e >= 0) {
+                    T.sp -= 1;
+                    bvh_interior3<BLOCK>(T, st, e, recs, fast, p.stack_slots, visits);
+                    if (T.sp == 0) T.sp = -1;
+                }
+            }
+            // leaf sub-step
+            if (T.sp > 0) {
+                const int e = st[(T.sp - 1) * BLOCK];
+                if (e < 0) {
+                    T.sp -= 1;
+                    bvh_leaf3(T, e, p.nodes, p.tri, tests);
+                    if (T.sp == 0) T.sp = -1;
+                }
+            }
+            const unsigned long long fin = __ballot(T.sp < 0);
+            if (!__any(T.sp > 0) || __popcll(fin) >= (unsigned)THRESH) break;
+        }
+    }
+    flush_counters(L, p);
+    unsigned long long t = tests, v = visits;
+    for (int off = 32; off > 0; off >>= 1) {
+        t += __shfl_xor(t, off);
+        v += __shfl_xor(v, off);
+    }
+    if (lane_id() == 0) {
+        atomicAdd(p.seg_counter + 1, t);  // leaf triangle tests
+        atomicAdd(p.seg_counter + 2, v);  // interior node visits (diagnostic)
+    }
+}
+
 // Division check for div_mk (test hook): n, d drawn from the ranges above.
 __global__ void div_check_kernel(uint32_t seed, unsigned long long count, unsigned long long* bad,
                                  uint32_t* first) {
@@ -1074,13 +1236,13 @@ __global__ void div_check_kernel(uint32_t seed, unsigned long long count, unsign
         uint32_t g = h * 747796405u + 2891336453u;
         g = ((g >> ((g >> 28u) + 4u)) ^ g) * 277803737u;
         g ^= g >> 22;
-        // n: |n| in [2^-60, 2^60], random sign/mantissa; d: |d| in [2^-20, 1]
+        // n: |n| in [2^-60, 2^60], random sign/mantissa; d: |d| in [1e-6, 2]
         const uint32_t ne = 127 - 60 + (h % 121u);
         const float n = __uint_as_float((h & 0x80000000u) | (ne << 23) | (g & 0x7fffffu));
-        const uint32_t de = 127 - 20 + ((g >> 23) % 21u);
+        const uint32_t de = 127 - 20 + ((g >> 23) % 22u);
         float d = __uint_as_float(((g << 8) & 0x80000000u) | (de << 23) | ((h * 2246822519u) & 0x7fffffu));
         if (fabsf(d) < 1e-6f) d = copysignf(1e-6f, d);
-        if (fabsf(d) > 1.0f) d = copysignf(1.0f, d);
+        if (fabsf(d) > 2.0f) d = copysignf(2.0f, d);
         const float y = 1.0f / d;
         const float q = div_mk(n, d, y);
         const float ref = n / d;
@@ -1318,6 +1480,7 @@ struct rt2_scene {
     rt2_node* d_nodes = nullptr;
     float4* d_recs = nullptr;                   // BVH v2 child-pair records
     int bvh_root = 0;                           // BVH v2 stack entry of node 0
+    int recs_ok = 0;                            // BVH v3 fast-path precondition on the boxes
     unsigned long long* d_counters = nullptr;  // [0] item counter, [1] segments
     unsigned long long samples = 0, tests_per_seg = 0;
     int variant = 0;
@@ -1483,6 +1646,13 @@ extern "C" int rt2_scene_create(const rt2_triangle* tris, int32_t n_tris, const 
             delete s;
             return -1;
         }
+        // the first three float4 of a record are box coordinates (the 4th: stack entries)
+        s->recs_ok = 1;
+        for (size_t i = 0; i < rec.size(); i++) {
+            if (i % 4 == 3) continue;
+            for (float c : {rec[i].x, rec[i].y, rec[i].z, rec[i].w})
+                if (!(c == 0.0f || (std::fabs(c) >= 0x1p-37f && std::fabs(c) <= 0x1p59f))) s->recs_ok = 0;
+        }
         HIPCHECK(hipMalloc(&s->d_recs, rec.size() * sizeof(float4)));
         HIPCHECK(hipMemcpy(s->d_recs, rec.data(), rec.size() * sizeof(float4), hipMemcpyHostToDevice));
     }
@@ -1532,7 +1702,7 @@ namespace {
 constexpr int kTileTris = 1024;  // 48 KiB of LDS per tile
 
 // Kernel variants (rt2_scene_set_variant); 0 = auto = the default below.
-enum Kind : int { K_RESIDENT = 0, K_TILED = 1, K_SMEM = 2, K_BVH = 3, K_BVH2 = 4 };
+enum Kind : int { K_RESIDENT = 0, K_TILED = 1, K_SMEM = 2, K_BVH = 3, K_BVH2 = 4, K_BVH3 = 5 };
 struct Variant {
     int kind;
     int block;
@@ -1551,6 +1721,8 @@ hipError_t launch_t(const RenderParams& p, int blocks, size_t lds, hipStream_t s
         hipLaunchKernelGGL((render_bvh<BLOCK>), dim3(blocks), dim3(BLOCK), lds, st, p);
     else if constexpr (KIND == K_BVH2)
         hipLaunchKernelGGL((render_bvh2<BLOCK, MT>), dim3(blocks), dim3(BLOCK), lds, st, p);
+    else if constexpr (KIND == K_BVH3)
+        hipLaunchKernelGGL((render_bvh3<BLOCK, MT>), dim3(blocks), dim3(BLOCK), lds, st, p);
     else
         hipLaunchKernelGGL((render_resident<BLOCK, MT, UNROLL>), dim3(blocks), dim3(BLOCK), lds, st, p);
     return hipGetLastError();
@@ -1565,6 +1737,8 @@ hipError_t occ_t(int* occ, size_t lds) {
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_bvh<BLOCK>, BLOCK, lds);
     else if constexpr (KIND == K_BVH2)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_bvh2<BLOCK, MT>, BLOCK, lds);
+    else if constexpr (KIND == K_BVH3)
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_bvh3<BLOCK, MT>, BLOCK, lds);
     else
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_resident<BLOCK, MT, UNROLL>, BLOCK, lds);
 }
@@ -1617,11 +1791,15 @@ const Variant kVariants[] = {
     RT2_VARIANT(K_BVH2, 128, 16, 1, "bvh2/128/t16"),                 // 43
     RT2_VARIANT(K_BVH2, 64, 16, 1, "bvh2/64/t16"),                   // 44
     RT2_VARIANT(K_BVH2, 256, 1, 1, "bvh2/256/t1"),                   // 45
+    RT2_VARIANT(K_BVH3, 256, 16, 1, "bvh3/256/t16"),                 // 46
+    RT2_VARIANT(K_BVH3, 256, 8, 1, "bvh3/256/t8"),                   // 47
+    RT2_VARIANT(K_BVH3, 256, 24, 1, "bvh3/256/t24"),                 // 48
+    RT2_VARIANT(K_BVH3, 128, 16, 1, "bvh3/128/t16"),                 // 49
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr size_t kResidentMaxBytes = 112 * 1024;
 constexpr int kSmemMaxTris = 16384;
-constexpr int kDefaultBvhVariant = 40;
+constexpr int kDefaultBvhVariant = 46;
 }  // namespace
 
 extern "C" const char* rt2_variant_name(int v) { return v >= 0 && v < kNumVariants ? kVariants[v].name : nullptr; }
@@ -1718,10 +1896,10 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     // auto: scalar-path kernel for small scenes (config B: 1,208 triangles),
     // LDS-tiled sweep for large ones (config C/E: 100k-1M triangles)
     if (s->traversal == RT2_TRAVERSAL_BVH) {
-        if (vi <= 0 || vi >= kNumVariants || (kVariants[vi].kind != K_BVH && kVariants[vi].kind != K_BVH2))
+        if (vi <= 0 || vi >= kNumVariants || kVariants[vi].kind < K_BVH)
             vi = kDefaultBvhVariant;
     } else {
-        if (vi <= 0 || vi >= kNumVariants || kVariants[vi].kind == K_BVH || kVariants[vi].kind == K_BVH2)
+        if (vi <= 0 || vi >= kNumVariants || kVariants[vi].kind >= K_BVH)
             vi = s->n_tris <= kSmemMaxTris ? 0 : 2;
         if (kVariants[vi].kind == K_RESIDENT && !fits) vi = 2;  // a resident variant cannot hold this scene
     }
@@ -1731,11 +1909,12 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
         lds = (size_t)3 * sizeof(float4) * kTileTris;
     else if (V.kind == K_RESIDENT)
         lds = resident_bytes;
-    else if (V.kind == K_BVH || V.kind == K_BVH2)
+    else if (V.kind >= K_BVH)
         lds = (size_t)p.stack_slots * V.block * sizeof(int);
     p.bvh_recs = s->d_recs;
     p.bvh_root = s->bvh_root;
-    s->last_kind = V.kind == K_BVH2 ? K_BVH : V.kind;
+    p.recs_ok = s->recs_ok;
+    s->last_kind = V.kind >= K_BVH ? K_BVH : V.kind;
     int occ = 0;
     HIPCHECK(V.occupancy(&occ, lds));
     occ = std::max(occ, 1);

@@ -10,8 +10,9 @@ TAG=$1
 shift
 run() {
   local name=$1
-  shift
-  timeout -k 10 300 rocprofv3 --pmc $1 --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/pmcp_${TAG}_$name" -o run \
+  local counters=$2
+  shift 2
+  timeout -k 10 300 rocprofv3 --pmc $counters --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/pmcp_${TAG}_$name" -o run \
     -- python3 "$@" > "$GRAFT_REPO_ROOT/gpurun_out/pmcp_${TAG}_$name.log" 2>&1
 }
 ARGS=("$@")

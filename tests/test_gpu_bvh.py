@@ -90,7 +90,9 @@ def test_bvh_requires_nodes_and_validates(rt2mod, torch_cuda):
         rt2mod.Scene(triangles=sd.triangles(), materials=sd.materials(), nodes=nodes)
 
 
-BVH2_VARIANTS = [40, 41, 42, 43, 44, 45]  # render_bvh2: child-pair records, Markstein slabs, while-while
+# render_bvh2 (child-pair records, Markstein slabs, while-while) and
+# render_bvh3 (+ wave-uniform fast slab path, fused interior/leaf sub-steps)
+BVH2_VARIANTS = [40, 41, 42, 43, 44, 45, 46, 47, 48, 49]
 
 
 def test_markstein_slab_division(rt2mod, torch_cuda):
@@ -123,10 +125,11 @@ def test_bvh2_large_mesh_and_diverse(rt2mod, oraclemod, config_scene, torch_cuda
     sd, spec = config_scene("C")
     u = rt2mod.offline_uniforms(96, 54, spec.bounces, 4, sd.num_triangles)
     scene = bvh_scene(rt2mod, sd)
-    scene.set_variant(40)
-    img = scene.render_host(u, 0, 1)
-    ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(54), 0, 1, "bvh")
-    assert_exact(img, ref, "bvh2 config C")
+    for v in (40, 46):
+        scene.set_variant(v)
+        img = scene.render_host(u, 0, 1)
+        ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(54), 0, 1, "bvh")
+        assert_exact(img, ref, f"variant {v} config C")
     M = rt2mod.Material
     sd = rt2mod.SceneData()
     ids = [sd.add_material(m) for m in (M.diffuse((1, 0, 0)), M.diffuse((0, 1, 0)), M.diffuse((1, 1, 1)),
@@ -137,17 +140,18 @@ def test_bvh2_large_mesh_and_diverse(rt2mod, oraclemod, config_scene, torch_cuda
     sd.build_bvh()
     u = rt2mod.offline_uniforms(80, 60, 12, 3, sd.num_triangles)
     scene = bvh_scene(rt2mod, sd)
-    scene.set_variant(40)
-    img = scene.render_host(u, 0, 2)
     ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(60), 0, 2, "bvh")
-    assert_exact(img, ref, "bvh2 diverse")
+    for v in (40, 46):
+        scene.set_variant(v)
+        img = scene.render_host(u, 0, 2)
+        assert_exact(img, ref, f"variant {v} diverse")
 
 
 def test_bvh2_big_leaves_and_single_node(rt2mod, oraclemod, torch_cuda):
     """Leaves of > 30 triangles take the node-array lookup; a one-node BVH is a leaf root."""
     M = rt2mod.Material
     rng = np.random.default_rng(5)
-    for n_tris in (1, 40, 300):
+    for n_tris, tiny in ((1, False), (40, False), (300, False), (300, True)):
         sd = rt2mod.SceneData()
         sd.add_material(M.diffuse((0.8, 0.8, 0.8)))
         sd.add_material(M.light((1, 1, 1), 5.0))
@@ -155,6 +159,9 @@ def test_bvh2_big_leaves_and_single_node(rt2mod, oraclemod, torch_cuda):
         for i in range(n_tris):
             sd.add_triangle(tuple(a[i]), tuple(a[i] + rng.uniform(-1, 1, 3)), tuple(a[i] + rng.uniform(-1, 1, 3)),
                             i % 2)
+        if tiny:  # a box coordinate of 1e-30 disables bvh3's fast slab path (IEEE slabs)
+            sd.add_triangle((1e-30, 4.0, -5.0), (1.0, 4.0, -5.0), (0.5, 5.0, -5.0), 0)
+            n_tris += 1
         sd.build_bvh()
         nodes = sd.nodes().copy()
         # one flat leaf over everything: exercises the count-31 escape and a leaf root
@@ -165,8 +172,9 @@ def test_bvh2_big_leaves_and_single_node(rt2mod, oraclemod, torch_cuda):
         for nd in (nodes, flat):
             scene = rt2mod.Scene(triangles=sd.triangles(), materials=sd.materials(), nodes=nd)
             scene.set_traversal("bvh")
-            scene.set_variant(40)
             u = rt2mod.offline_uniforms(48, 32, 6, 2, n_tris)
-            img = scene.render_host(u, 0, 1)
             acc, _, _, _ = oraclemod.render(sd.triangles(), sd.materials(), u, np.arange(32), 0, 1, "bvh", nodes=nd)
-            assert_exact(img, acc[..., :3], f"bvh2 n={n_tris} nodes={len(nd)}")
+            for v in (40, 46):
+                scene.set_variant(v)
+                img = scene.render_host(u, 0, 1)
+                assert_exact(img, acc[..., :3], f"variant {v} n={n_tris} nodes={len(nd)}")
