@@ -206,6 +206,13 @@ int rt2_scene_set_variant(rt2_scene* scene, int variant);
 enum { RT2_TRAVERSAL_BRUTE = 0, RT2_TRAVERSAL_BVH = 1 };
 int rt2_scene_set_traversal(rt2_scene* scene, int traversal);
 
+/* Work-item shape for frame_count > 1 (default 1): the render hands out
+ * (frame, pixel) items frame-major and adds the frames in order afterwards,
+ * instead of one whole pixel (all frames) per item — a shorter tail at the end
+ * of each launch.  Results are bit-identical either way; costs
+ * frame_count * pixels * 16 B of device scratch per scene. */
+int rt2_scene_set_frame_split(rt2_scene* scene, int enable);
+
 /* ------------------------------------------------------------------------
  * (2) Host surface
  * ---------------------------------------------------------------------- */

@@ -49,7 +49,10 @@ struct RenderParams {
     float cam[3], vpRight[3], vpUp[3], vpFront[3], pixR[3], pixU[3], defR[3], defU[3];
     uint32_t frame_begin, frame_count;
     int tile_rows, rank, nranks;
-    unsigned long long n_items;
+    unsigned long long n_items;  // work items: pixels, or frames x pixels when frame_split
+    unsigned long long n_pix;    // pixels of the shard
+    int frame_split;             // 1: item = (frame, pixel), frame-major; colours -> frame_buf
+    float4* frame_buf;           // frame_split: [frame_count][n_pix] per-frame colours
     float4* accum;
     uint4* accum8;
     unsigned long long* item_counter;
@@ -453,11 +456,14 @@ __device__ __forceinline__ void advance(Lane& L, const RenderParams& p) {
             if (need) {
                 unsigned long long it = base + lanes_below(m);
                 if (it < p.n_items) {
-                    L.item = (uint32_t)it;
+                    // frame_split: item = frame * n_pix + pixel (frame-major), so the
+                    // last items of a launch are single pixel-frames
+                    const uint32_t f = p.frame_split ? (uint32_t)(it / p.n_pix) : 0u;
+                    L.item = (uint32_t)(it - (unsigned long long)f * p.n_pix);
                     int lr = (int)(L.item / (uint32_t)p.W);
                     L.x = (int)(L.item - (uint32_t)lr * (uint32_t)p.W);
                     L.y = shard_row(lr, p.tile_rows, p.rank, p.nranks);
-                    L.frame = 0;
+                    L.frame = f;
                     L.st = ST_NEW_FRAME;
                 } else {
                     L.st = ST_DONE;
@@ -507,6 +513,11 @@ __device__ __forceinline__ void end_path(Lane& L, const RenderParams& p) {
     }
     f3 c = divs(L.colorCum, (float)p.R);
     c = mk(srgb1(aces1(c.x)), srgb1(aces1(c.y)), srgb1(aces1(c.z)));
+    if (p.frame_split) {  // frame_accumulate adds the frames in order afterwards
+        p.frame_buf[(size_t)L.frame * p.n_pix + L.item] = make_float4(c.x, c.y, c.z, 0.0f);
+        L.st = ST_NEED_ITEM;
+        return;
+    }
     // accumulate this frame in frame order: acc = acc + colour
     const float4 a = p.accum[L.item];
     p.accum[L.item] = make_float4(a.x + c.x, a.y + c.y, a.z + c.z, 0.0f);
@@ -1083,8 +1094,10 @@ struct TravState3 {
     int bi;
     bool fast;  // no skipped axis, Markstein preconditions hold
     SlabRay R;
+    double yx, yy, yz;  // DIV64: RN64(1/d) on unskipped axes
 };
 
+template <int DIV>
 __device__ __forceinline__ void begin_segment3(Lane& L, TravState3& T, int* st, int root) {
     L.bounce += 1;
     L.segs += 1;
@@ -1097,8 +1110,15 @@ __device__ __forceinline__ void begin_segment3(Lane& L, TravState3& T, int* st, 
     T.R.sy = L.d.y < 1e-6f && L.d.y > -1e-6f;
     T.R.sz = L.d.z < 1e-6f && L.d.z > -1e-6f;
     T.R.y = mk(T.R.sx ? 0.0f : 1.0f / L.d.x, T.R.sy ? 0.0f : 1.0f / L.d.y, T.R.sz ? 0.0f : 1.0f / L.d.z);
-    T.fast = !(T.R.sx || T.R.sy || T.R.sz) && mk_coord_ok(L.o.x) && mk_coord_ok(L.o.y) && mk_coord_ok(L.o.z) &&
-             fabsf(L.d.x) <= 2.0f && fabsf(L.d.y) <= 2.0f && fabsf(L.d.z) <= 2.0f;
+    if constexpr (DIV == 1) {
+        T.fast = !(T.R.sx || T.R.sy || T.R.sz);
+        T.yx = 1.0 / (double)L.d.x;
+        T.yy = 1.0 / (double)L.d.y;
+        T.yz = 1.0 / (double)L.d.z;
+    } else {
+        T.fast = !(T.R.sx || T.R.sy || T.R.sz) && mk_coord_ok(L.o.x) && mk_coord_ok(L.o.y) &&
+                 mk_coord_ok(L.o.z) && fabsf(L.d.x) <= 2.0f && fabsf(L.d.y) <= 2.0f && fabsf(L.d.z) <= 2.0f;
+    }
     st[0] = root;
     T.sp = 1;
 }
@@ -1122,7 +1142,31 @@ __device__ __forceinline__ float slab_fast(const SlabRay& R, float b0x, float b0
     return (tMin >= tMax || tMax < 0.0f) ? 1e38f : tMin;
 }
 
-template <int BLOCK>
+// Exact RN32(n/d) through binary64: with yd = RN64(1/d),
+// RN32(RN64(n*yd)) = RN32(n/d) for every float n and normal d: n*yd is within
+// 2^-52 relative of n/d, i.e. 2^-28 ulp32, while a quotient of two floats is
+// never closer than 2^-25 ulp32 to a binary32 rounding boundary (midpoint).
+__device__ __forceinline__ float div64(float n, double yd) { return (float)((double)n * yd); }
+
+__device__ __forceinline__ float slab64(const TravState3& T, float b0x, float b0y, float b0z, float b1x, float b1y,
+                                        float b1z) {
+    float tMin = -1e32f, tMax = 1e32f;
+#define RT2_SLAB64(B0, B1, O, Y)                                \
+    {                                                           \
+        float t0 = div64(B0 - O, Y);                            \
+        float t1 = div64(B1 - O, Y);                            \
+        if (t0 > t1) { const float t_ = t0; t0 = t1; t1 = t_; } \
+        if (tMin < t0) tMin = t0;                               \
+        if (tMax > t1) tMax = t1;                               \
+    }
+    RT2_SLAB64(b0x, b1x, T.R.o.x, T.yx)
+    RT2_SLAB64(b0y, b1y, T.R.o.y, T.yy)
+    RT2_SLAB64(b0z, b1z, T.R.o.z, T.yz)
+#undef RT2_SLAB64
+    return (tMin >= tMax || tMax < 0.0f) ? 1e38f : tMin;
+}
+
+template <int BLOCK, int DIV>
 __device__ __forceinline__ void bvh_interior3(TravState3& T, int* st, int e, const float4* __restrict__ recs,
                                               bool fast, int stack_slots, uint32_t& visits) {
     visits++;
@@ -1130,7 +1174,10 @@ __device__ __forceinline__ void bvh_interior3(TravState3& T, int* st, int e, con
     const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
     const float4 r3 = rp[3];
     float dA, dB;
-    if (fast) {
+    if (fast && DIV == 1) {
+        dA = slab64(T, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y);
+        dB = slab64(T, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w);
+    } else if (fast) {
         dA = slab_fast(T.R, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y);
         dB = slab_fast(T.R, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w);
     } else {
@@ -1164,7 +1211,7 @@ __device__ __forceinline__ void bvh_leaf3(TravState3& T, int e, const rt2_node* 
     }
 }
 
-template <int BLOCK, int THRESH>
+template <int BLOCK, int THRESH, int DIV>
 __global__ __launch_bounds__(BLOCK) void render_bvh3(RenderParams p) {
     extern __shared__ int bvh_stack[];
     int* st = bvh_stack + threadIdx.x;
@@ -1176,6 +1223,7 @@ __global__ __launch_bounds__(BLOCK) void render_bvh3(RenderParams p) {
     T.best = T.bestK = 1e38f;
     T.bi = -1;
     T.fast = true;
+    T.yx = T.yy = T.yz = 0.0;
     uint32_t tests = 0, visits = 0;
     for (;;) {
         if (T.sp < 0) {
@@ -1183,16 +1231,16 @@ __global__ __launch_bounds__(BLOCK) void render_bvh3(RenderParams p) {
             T.sp = 0;
         }
         advance(L, p);
-        if (L.st == ST_TRACE && T.sp == 0) begin_segment3(L, T, st, p.bvh_root);
+        if (L.st == ST_TRACE && T.sp == 0) begin_segment3<DIV>(L, T, st, p.bvh_root);
         if (!__any(T.sp > 0)) break;
-        const bool fast = p.recs_ok && __all(T.fast || T.sp <= 0);
+        const bool fast = (DIV == 1 || p.recs_ok) && __all(T.fast || T.sp <= 0);
         for (;;) {
             // interior sub-step
             if (T.sp > 0) {
                 const int e = st[(T.sp - 1) * BLOCK];
                 if (e >= 0) {
                     T.sp -= 1;
-                    bvh_interior3<BLOCK>(T, st, e, recs, fast, p.stack_slots, visits);
+                    bvh_interior3<BLOCK, DIV>(T, st, e, recs, fast, p.stack_slots, visits);
                     if (T.sp == 0) T.sp = -1;
                 }
             }
@@ -1218,11 +1266,15 @@ __global__ __launch_bounds__(BLOCK) void render_bvh3(RenderParams p) {
     if (lane_id() == 0) {
         atomicAdd(p.seg_counter + 1, t);  // leaf triangle tests
         atomicAdd(p.seg_counter + 2, v);  // interior node visits (diagnostic)
+        // wave finish-time spread (diagnostic): [6] earliest, [7] latest wave end, 10 ns ticks
+        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+        atomicMin(p.seg_counter + 5, t_end);
+        atomicMax(p.seg_counter + 6, t_end);
     }
 }
 
 // Division check for div_mk (test hook): n, d drawn from the ranges above.
-__global__ void div_check_kernel(uint32_t seed, unsigned long long count, unsigned long long* bad,
+__global__ void div_check_kernel(uint32_t seed, unsigned long long count, int mode, unsigned long long* bad,
                                  uint32_t* first) {
     const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
     unsigned long long nbad = 0;
@@ -1237,14 +1289,14 @@ __global__ void div_check_kernel(uint32_t seed, unsigned long long count, unsign
         g = ((g >> ((g >> 28u) + 4u)) ^ g) * 277803737u;
         g ^= g >> 22;
         // n: |n| in [2^-60, 2^60], random sign/mantissa; d: |d| in [1e-6, 2]
-        const uint32_t ne = 127 - 60 + (h % 121u);
+        // mode 1 (div64): any finite n, subnormals included
+        const uint32_t ne = mode == 1 ? (h % 255u) : 127 - 60 + (h % 121u);
         const float n = __uint_as_float((h & 0x80000000u) | (ne << 23) | (g & 0x7fffffu));
         const uint32_t de = 127 - 20 + ((g >> 23) % 22u);
         float d = __uint_as_float(((g << 8) & 0x80000000u) | (de << 23) | ((h * 2246822519u) & 0x7fffffu));
         if (fabsf(d) < 1e-6f) d = copysignf(1e-6f, d);
         if (fabsf(d) > 2.0f) d = copysignf(2.0f, d);
-        const float y = 1.0f / d;
-        const float q = div_mk(n, d, y);
+        const float q = mode == 1 ? div64(n, 1.0 / (double)d) : div_mk(n, d, 1.0f / d);
         const float ref = n / d;
         if (__float_as_uint(q) != __float_as_uint(ref)) {
             nbad++;
@@ -1390,6 +1442,25 @@ __global__ __launch_bounds__(BLOCK) void render_basic(RenderParams p) {
     }
 }
 
+// frame_split epilogue: acc += colour_f for f = 0 .. F-1 in frame order (the
+// same float sums as the in-lane accumulation), plus the unorm8 path.
+__global__ void frame_accumulate(const float4* __restrict__ fb, unsigned long long n_pix, uint32_t frames,
+                                 float4* __restrict__ acc, uint4* __restrict__ acc8) {
+    const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_pix) return;
+    float4 a = acc[i];
+    uint4 q = acc8 ? acc8[i] : make_uint4(0, 0, 0, 0);
+    for (uint32_t f = 0; f < frames; f++) {
+        const float4 c = fb[(size_t)f * n_pix + i];
+        a = make_float4(a.x + c.x, a.y + c.y, a.z + c.z, 0.0f);
+        q.x += (uint32_t)(clampf(c.x, 0.0f, 1.0f) * 255.0f + 0.5f);
+        q.y += (uint32_t)(clampf(c.y, 0.0f, 1.0f) * 255.0f + 0.5f);
+        q.z += (uint32_t)(clampf(c.z, 0.0f, 1.0f) * 255.0f + 0.5f);
+    }
+    acc[i] = a;
+    if (acc8) acc8[i] = q;
+}
+
 // Pre-transform: RTXTriangle (80 B) -> {a, e0, e1, n} (48 B) + material index.
 __global__ void prep_triangles(const rt2_triangle* tris, int n, float4* out, int* mtl) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1479,8 +1550,11 @@ struct rt2_scene {
     rt2_material* d_mats = nullptr;
     rt2_node* d_nodes = nullptr;
     float4* d_recs = nullptr;                   // BVH v2 child-pair records
+    float4* d_fb = nullptr;                     // frame_split scratch (per-frame colours)
+    size_t fb_bytes = 0;
     int bvh_root = 0;                           // BVH v2 stack entry of node 0
     int recs_ok = 0;                            // BVH v3 fast-path precondition on the boxes
+    int split_frames = 1;                       // frame-major (frame, pixel) items when F > 1
     unsigned long long* d_counters = nullptr;  // [0] item counter, [1] segments
     unsigned long long samples = 0, tests_per_seg = 0;
     int variant = 0;
@@ -1576,6 +1650,15 @@ static int bvh_records(const rt2_node* nodes, int n_nodes, std::vector<float4>& 
     }
     root = enc(0);
     return n_int;
+}
+
+extern "C" int rt2_scene_set_frame_split(rt2_scene* s, int enable) {
+    if (!s) {
+        rt2h::set_error("rt2_scene_set_frame_split: null scene");
+        return -1;
+    }
+    s->split_frames = enable ? 1 : 0;
+    return 0;
 }
 
 extern "C" int rt2_scene_set_traversal(rt2_scene* s, int traversal) {
@@ -1675,6 +1758,7 @@ extern "C" void rt2_scene_destroy(rt2_scene* s) {
     (void)hipFree(s->d_mats);
     (void)hipFree(s->d_nodes);
     (void)hipFree(s->d_recs);
+    (void)hipFree(s->d_fb);
     (void)hipFree(s->d_counters);
     delete s;
 }
@@ -1722,7 +1806,7 @@ hipError_t launch_t(const RenderParams& p, int blocks, size_t lds, hipStream_t s
     else if constexpr (KIND == K_BVH2)
         hipLaunchKernelGGL((render_bvh2<BLOCK, MT>), dim3(blocks), dim3(BLOCK), lds, st, p);
     else if constexpr (KIND == K_BVH3)
-        hipLaunchKernelGGL((render_bvh3<BLOCK, MT>), dim3(blocks), dim3(BLOCK), lds, st, p);
+        hipLaunchKernelGGL((render_bvh3<BLOCK, MT % 1000, MT / 1000>), dim3(blocks), dim3(BLOCK), lds, st, p);
     else
         hipLaunchKernelGGL((render_resident<BLOCK, MT, UNROLL>), dim3(blocks), dim3(BLOCK), lds, st, p);
     return hipGetLastError();
@@ -1738,7 +1822,8 @@ hipError_t occ_t(int* occ, size_t lds) {
     else if constexpr (KIND == K_BVH2)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_bvh2<BLOCK, MT>, BLOCK, lds);
     else if constexpr (KIND == K_BVH3)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_bvh3<BLOCK, MT>, BLOCK, lds);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_bvh3<BLOCK, MT % 1000, MT / 1000>, BLOCK,
+                                                            lds);
     else
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_resident<BLOCK, MT, UNROLL>, BLOCK, lds);
 }
@@ -1795,6 +1880,8 @@ const Variant kVariants[] = {
     RT2_VARIANT(K_BVH3, 256, 8, 1, "bvh3/256/t8"),                   // 47
     RT2_VARIANT(K_BVH3, 256, 24, 1, "bvh3/256/t24"),                 // 48
     RT2_VARIANT(K_BVH3, 128, 16, 1, "bvh3/128/t16"),                 // 49
+    RT2_VARIANT(K_BVH3, 256, 1016, 1, "bvh3/256/t16/div64"),         // 50
+    RT2_VARIANT(K_BVH3, 256, 1008, 1, "bvh3/256/t8/div64"),          // 51
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr size_t kResidentMaxBytes = 112 * 1024;
@@ -1853,8 +1940,9 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     p.tile_rows = sh.tile_rows;
     p.rank = sh.rank;
     p.nranks = sh.nranks;
-    p.n_items = (unsigned long long)rows * (unsigned long long)p.W;
-    if (p.n_items >= 0xffffffffull) {
+    p.n_pix = (unsigned long long)rows * (unsigned long long)p.W;
+    p.n_items = p.n_pix;
+    if (p.n_pix >= 0xffffffffull) {
         rt2h::set_error("rt2_render: more than 2^32-1 pixels in one shard");
         return -1;
     }
@@ -1890,6 +1978,21 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
         s->tests_per_seg = (unsigned long long)s->n_tris;
         return 0;
     }
+    // several frames: frame-major (frame, pixel) items into a scratch buffer,
+    // then frame_accumulate (finer work items: a shorter tail)
+    if (frame_count > 1 && s->split_frames && p.n_pix * frame_count < 0xffffffffull) {
+        const size_t need = (size_t)p.n_pix * frame_count * sizeof(float4);
+        if (need > s->fb_bytes) {
+            if (s->d_fb) HIPCHECK(hipFree(s->d_fb));
+            s->d_fb = nullptr;
+            s->fb_bytes = 0;
+            HIPCHECK(hipMalloc(&s->d_fb, need));
+            s->fb_bytes = need;
+        }
+        p.frame_split = 1;
+        p.frame_buf = s->d_fb;
+        p.n_items = p.n_pix * frame_count;
+    }
     const size_t resident_bytes = (size_t)3 * sizeof(float4) * (size_t)std::max(s->n_tris, 1);
     const bool fits = resident_bytes <= kResidentMaxBytes;
     int vi = s->variant;
@@ -1924,7 +2027,12 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     s->last_variant = vi;
     HIPCHECK(V.launch(p, (int)blocks, lds, st));
     HIPCHECK(hipGetLastError());
-    s->samples += p.n_items * (unsigned long long)p.R * (unsigned long long)frame_count;
+    if (p.frame_split) {
+        hipLaunchKernelGGL(frame_accumulate, dim3((unsigned)((p.n_pix + 255) / 256)), dim3(256), 0, st, p.frame_buf,
+                           p.n_pix, frame_count, p.accum, p.accum8);
+        HIPCHECK(hipGetLastError());
+    }
+    s->samples += p.n_pix * (unsigned long long)p.R * (unsigned long long)frame_count;
     s->tests_per_seg = (unsigned long long)s->n_tris;
     return 0;
 }
@@ -2060,16 +2168,17 @@ extern "C" int rt2_device_rcp_check(uint32_t lo, uint32_t hi, int variant, unsig
     return 0;
 }
 
-// Not in rt2.h (test hook): div_mk against IEEE division on `count` random
-// (n, d) pairs of the ranges bvh_step uses it on.
-extern "C" int rt2_device_div_check(uint32_t seed, unsigned long long count, unsigned long long* mismatches,
-                                    uint32_t* first_bad) {
+// Not in rt2.h (test hook): div_mk (mode 0) or div64 (mode 1) against IEEE
+// division on `count` random (n, d) pairs of the ranges the kernels use them on.
+extern "C" int rt2_device_div_check(uint32_t seed, unsigned long long count, int mode,
+                                    unsigned long long* mismatches, uint32_t* first_bad) {
     unsigned long long* d = nullptr;
     HIPCHECK(hipMalloc(&d, 16));
     HIPCHECK(hipMemset(d, 0, 8));
     uint32_t init = 0xffffffffu;
     HIPCHECK(hipMemcpy((char*)d + 8, &init, 4, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(div_check_kernel, dim3(8192), dim3(256), 0, 0, seed, count, d, (uint32_t*)((char*)d + 8));
+    hipLaunchKernelGGL(div_check_kernel, dim3(8192), dim3(256), 0, 0, seed, count, mode, d,
+                       (uint32_t*)((char*)d + 8));
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipMemcpy(mismatches, d, 8, hipMemcpyDeviceToHost));
     HIPCHECK(hipMemcpy(first_bad, (char*)d + 8, 4, hipMemcpyDeviceToHost));

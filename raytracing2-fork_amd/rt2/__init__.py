@@ -139,7 +139,7 @@ assert TRI_DTYPE.itemsize == 80 and MAT_DTYPE.itemsize == 96 and NODE_DTYPE.item
 EXPORTED = [
     "rt2_last_error", "rt2_abi_version", "rt2_scene_create", "rt2_scene_destroy", "rt2_shard_rows",
     "rt2_shard_row", "rt2_render", "rt2_render_host", "rt2_resolve_rgba32f", "rt2_resolve_rgb8_reference",
-    "rt2_scene_stats", "rt2_scene_set_variant", "rt2_scene_set_traversal", "rt2_sd_create", "rt2_sd_destroy", "rt2_sd_load_obj_folder",
+    "rt2_scene_stats", "rt2_scene_set_variant", "rt2_scene_set_traversal", "rt2_scene_set_frame_split", "rt2_sd_create", "rt2_sd_destroy", "rt2_sd_load_obj_folder",
     "rt2_sd_add_material", "rt2_sd_add_triangle", "rt2_sd_add_triangles", "rt2_sd_add_cornell_box", "rt2_sd_add_mirror_cornell_box",
     "rt2_sd_add_side_lit_cornell_box", "rt2_sd_add_sky_light_plane", "rt2_sd_add_cube",
     "rt2_sd_create_classic_cornell_box", "rt2_sd_create_diverse_cornell_box", "rt2_sd_build_bvh",
@@ -192,6 +192,7 @@ def lib() -> C.CDLL:
         "rt2_scene_stats": (C.c_int, [P, C.POINTER(Stats), C.c_int]),
         "rt2_scene_set_variant": (C.c_int, [P, C.c_int]),
         "rt2_scene_set_traversal": (C.c_int, [P, C.c_int]),
+        "rt2_scene_set_frame_split": (C.c_int, [P, C.c_int]),
         "rt2_sd_create": (P, []),
         "rt2_sd_destroy": (None, [P]),
         "rt2_sd_load_obj_folder": (C.c_int, [P, C.c_char_p]),
@@ -227,7 +228,7 @@ def lib() -> C.CDLL:
         "rt2_write_png": (C.c_int, [C.c_char_p, I32, I32, I32, P, I32]),
         "rt2_device_selftest": (C.c_int, [P, I32, P]),
         "rt2_device_rcp_check": (C.c_int, [U32, U32, C.c_int, C.POINTER(C.c_ulonglong), C.POINTER(U32)]),
-        "rt2_device_div_check": (C.c_int, [U32, C.c_ulonglong, C.POINTER(C.c_ulonglong), C.POINTER(U32)]),
+        "rt2_device_div_check": (C.c_int, [U32, C.c_ulonglong, C.c_int, C.POINTER(C.c_ulonglong), C.POINTER(U32)]),
         "rt2_variant_name": (C.c_char_p, [C.c_int]),
         "rt2_scene_diag": (C.c_int, [P, C.POINTER(C.c_ulonglong), C.POINTER(C.c_int)]),
     }
@@ -413,6 +414,10 @@ class Scene:
     def set_traversal(self, traversal: str) -> None:
         """"brute" (north-star kernel) or "bvh" (compute.glsl:410-460 on the uploaded nodes)."""
         _check(lib().rt2_scene_set_traversal(self._p, {"brute": 0, "bvh": 1}[traversal]), "set_traversal")
+
+    def set_frame_split(self, enable: bool) -> None:
+        """(frame, pixel) work items for multi-frame renders (rt2_scene_set_frame_split)."""
+        _check(lib().rt2_scene_set_frame_split(self._p, int(bool(enable))), "set_frame_split")
 
     def render(self, u: Uniforms, frame_begin: int, frame_count: int, sh: Shard, accum_ptr: int,
                accum8_ptr: int = 0, stream: int = 0) -> None:

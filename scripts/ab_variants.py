@@ -23,12 +23,14 @@ ap.add_argument("--height", type=int, default=0)
 ap.add_argument("--rays", type=int, default=0)
 ap.add_argument("--frames", type=int, default=0)
 ap.add_argument("--traversal", default="brute", choices=["brute", "bvh"])
+ap.add_argument("--no-split", action="store_true", help="whole-pixel items for F > 1")
 a = ap.parse_args()
 sd, spec = rt2.build_config_scene(a.config)
 W, H, R = a.width or spec.width, a.height or spec.height, a.rays or spec.rays
 u = rt2.offline_uniforms(W, H, spec.bounces, R, sd.num_triangles)
 scene = rt2.Scene(sd, 0)
 scene.set_traversal(a.traversal)
+scene.set_frame_split(not a.no_split)
 F = a.frames or spec.frames
 variants = [int(v) for v in a.variants.split(",")]
 times = {v: [] for v in variants}
@@ -49,7 +51,8 @@ for rnd in range(a.rounds):
         rt2.lib().rt2_scene_diag(scene._p, c, C.byref(lv))
         if a.traversal == "bvh":
             diag[v] = dict(segments=c[1], tests_per_segment=c[2] / max(c[1], 1),
-                           interior_visits_per_segment=c[3] / max(c[1], 1))
+                           interior_visits_per_segment=c[3] / max(c[1], 1),
+                           wave_end_spread_ms=(c[7] - c[6]) * 1e-5 if c[7] > c[6] else None)
         elif c[2]:
             diag[v] = dict(segments=c[1], groups=c[2], groups_with_survivor=c[3], exact_iters=c[4],
                            lane_survivors=c[5], frac_groups_exact=c[3] / c[2], exact_iters_per_group=c[4] / c[2],

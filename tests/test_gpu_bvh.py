@@ -92,17 +92,19 @@ def test_bvh_requires_nodes_and_validates(rt2mod, torch_cuda):
 
 # render_bvh2 (child-pair records, Markstein slabs, while-while) and
 # render_bvh3 (+ wave-uniform fast slab path, fused interior/leaf sub-steps)
-BVH2_VARIANTS = [40, 41, 42, 43, 44, 45, 46, 47, 48, 49]
+BVH2_VARIANTS = [40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51]
 
 
-def test_markstein_slab_division(rt2mod, torch_cuda):
-    """div_mk == IEEE n/d on 2^32 random pairs of the ranges bvh_step uses it on."""
+@pytest.mark.parametrize("mode", [0, 1])
+def test_exact_slab_division(rt2mod, torch_cuda, mode):
+    """div_mk (mode 0) / div64 (mode 1) == IEEE n/d on 2^32 random pairs of the
+    ranges the BVH kernels use them on."""
     import ctypes as C
     bad = C.c_ulonglong(0)
     first = C.c_uint32(0)
     for seed in (1, 2, 3, 4):
-        assert rt2mod.lib().rt2_device_div_check(seed, 1 << 30, C.byref(bad), C.byref(first)) == 0
-        assert bad.value == 0, f"seed {seed}: {bad.value} mismatches, first index {first.value}"
+        assert rt2mod.lib().rt2_device_div_check(seed, 1 << 30, mode, C.byref(bad), C.byref(first)) == 0
+        assert bad.value == 0, f"mode {mode} seed {seed}: {bad.value} mismatches, first index {first.value}"
 
 
 @pytest.mark.parametrize("variant", BVH2_VARIANTS)
@@ -125,7 +127,7 @@ def test_bvh2_large_mesh_and_diverse(rt2mod, oraclemod, config_scene, torch_cuda
     sd, spec = config_scene("C")
     u = rt2mod.offline_uniforms(96, 54, spec.bounces, 4, sd.num_triangles)
     scene = bvh_scene(rt2mod, sd)
-    for v in (40, 46):
+    for v in (40, 46, 50):
         scene.set_variant(v)
         img = scene.render_host(u, 0, 1)
         ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(54), 0, 1, "bvh")
@@ -141,7 +143,7 @@ def test_bvh2_large_mesh_and_diverse(rt2mod, oraclemod, config_scene, torch_cuda
     u = rt2mod.offline_uniforms(80, 60, 12, 3, sd.num_triangles)
     scene = bvh_scene(rt2mod, sd)
     ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(60), 0, 2, "bvh")
-    for v in (40, 46):
+    for v in (40, 46, 50):
         scene.set_variant(v)
         img = scene.render_host(u, 0, 2)
         assert_exact(img, ref, f"variant {v} diverse")
@@ -174,7 +176,7 @@ def test_bvh2_big_leaves_and_single_node(rt2mod, oraclemod, torch_cuda):
             scene.set_traversal("bvh")
             u = rt2mod.offline_uniforms(48, 32, 6, 2, n_tris)
             acc, _, _, _ = oraclemod.render(sd.triangles(), sd.materials(), u, np.arange(32), 0, 1, "bvh", nodes=nd)
-            for v in (40, 46):
+            for v in (40, 46, 50):
                 scene.set_variant(v)
                 img = scene.render_host(u, 0, 1)
                 assert_exact(img, acc[..., :3], f"variant {v} n={n_tris} nodes={len(nd)}")

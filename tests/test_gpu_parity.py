@@ -234,3 +234,23 @@ def test_bad_material_index_rejected(rt2mod, torch_cuda):
     sd.add_triangle((0, 0, 0), (1, 0, 0), (0, 1, 0), 5)
     with pytest.raises(rt2mod.RT2Error, match="material index"):
         rt2mod.Scene(sd, 0)
+
+
+@pytest.mark.parametrize("traversal", ["brute", "bvh"])
+def test_frame_split_identical(rt2mod, oraclemod, config_scene, torch_cuda, traversal):
+    """(frame, pixel) work items + frame_accumulate give the same bits as whole-pixel items."""
+    sd, spec = config_scene("B")
+    W, H, R, F = 96, 54, 4, 3
+    u = rt2mod.offline_uniforms(W, H, spec.bounces, R, sd.num_triangles)
+    out = {}
+    for split in (False, True):
+        scene = rt2mod.Scene(sd, 0)
+        scene.set_traversal(traversal)
+        scene.set_frame_split(split)
+        out[split] = scene.render_host(u, 2, F, rgb8=True)
+        st = scene.stats(reset=True)
+        assert st.samples == W * H * R * F
+    assert np.array_equal(out[False][0], out[True][0])
+    assert np.array_equal(out[False][1], out[True][1])
+    ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(H), 2, F, traversal)
+    assert_exact(out[True][0], ref, f"split {traversal}")
