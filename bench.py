@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--traversal", default="brute", choices=["brute", "bvh"],
                     help="brute = the north-star kernel (default); bvh = the reference's traversal on the GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-alt", action="store_true", help="skip timing the other traversal beside the headline")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target seconds per CPU baseline mode")
     return ap.parse_args()
 
@@ -77,15 +78,22 @@ def cpu_baseline(sd, spec, u, gpu_image, threads):
         oracle.render_pixels(tris, mats, u, pid % W, pid // W, 0, spec.frames, mode, nodes=nodes, threads=threads)
         dt = max(time.perf_counter() - t0, 1e-3) / nprobe
         n = int(max(threads, min(npx_all, args.cpu_seconds / dt)))
-        stride = max(1, npx_all // n)
-        pid = np.arange(stride // 2, npx_all, stride, dtype=np.int64)[:n]
+        pid = np.arange(n, dtype=np.int64) * npx_all // n  # n pixels spread evenly in raster order
         xs, ys = pid % W, pid // W
         t0 = time.perf_counter()
         acc, _, segs, tests = oracle.render_pixels(tris, mats, u, xs, ys, 0, spec.frames, mode, nodes=nodes,
                                                    threads=threads)
         dt = time.perf_counter() - t0
+        if dt < 0.4 * args.cpu_seconds and n < npx_all:  # the probe over-estimated: resize once
+            n = int(min(npx_all, n * args.cpu_seconds / max(dt, 1e-3)))
+            pid = np.arange(n, dtype=np.int64) * npx_all // n
+            xs, ys = pid % W, pid // W
+            t0 = time.perf_counter()
+            acc, _, segs, tests = oracle.render_pixels(tris, mats, u, xs, ys, 0, spec.frames, mode, nodes=nodes,
+                                                       threads=threads)
+            dt = time.perf_counter() - t0
         samples = len(pid) * spec.rays * spec.frames
-        res[mode] = dict(value=samples / dt / 1e6, pixels=int(len(pid)), stride=int(stride), seconds=dt,
+        res[mode] = dict(value=samples / dt / 1e6, pixels=int(len(pid)), seconds=dt,
                          segments_per_sample=segs / samples, tests_per_segment=tests / max(segs, 1))
         done[mode] = (ys, xs, acc / spec.frames)
     parity = None
@@ -216,15 +224,54 @@ def main():
     if os.path.exists(traffic_file):
         with open(traffic_file) as f:
             out["roofline"]["traffic"] = json.load(f).get("hbm_bytes_per_launch")
+    alt = "bvh" if args.traversal == "brute" else "brute"
+    # brute force over 100k+ triangles takes minutes per step: not timed beside BVH there
+    if world == 1 and not args.no_alt and (alt == "bvh" or sd.num_triangles <= 20000):
+        # the other closest-hit algorithm on the same workload, same timing
+        # bracket (reported beside the headline, never as `value`)
+        img_main = img.clone()
+        scene.set_traversal(alt)
+        scene.set_variant(0)
+        renderer.accum.zero_()
+        scene.render(u, 0, spec.frames, renderer.sh, renderer.accum.data_ptr(), 0, stream.cuda_stream)
+        torch.cuda.synchronize()
+        scene.stats(reset=True)
+        ev2 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
+        t1 = time.perf_counter()
+        for i in range(args.steps):
+            renderer.accum.zero_()
+            ev2[i][0].record(stream)
+            scene.render(u, 0, spec.frames, renderer.sh, renderer.accum.data_ptr(), 0, stream.cuda_stream)
+            ev2[i][1].record(stream)
+            rt2.resolve_rgba32f(renderer.accum.data_ptr(), renderer.rows * spec.width, spec.frames,
+                                renderer.image.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize()
+        el2 = time.perf_counter() - t1
+        st2 = scene.stats(reset=True)
+        ndiff = int((renderer.image[..., :3] != img_main[..., :3]).any(-1).sum().item())
+        d2 = (renderer.image[..., :3] - img_main[..., :3]).double()
+        out["alt_traversal"] = {
+            "traversal": alt, "value": round(samples_per_step * args.steps / el2 / 1e6, 3),
+            "ms_per_step": round(el2 / args.steps * 1e3, 3),
+            "kernel": KERNEL_NAMES[alt],
+            "kernel_ms": round(float(np.mean([a.elapsed_time(b) for a, b in ev2])), 3),
+            "segments_per_sample": round(st2.segments / (samples_per_step * args.steps), 4),
+            "tests_per_segment": round(st2.tests / max(st2.segments, 1), 3),
+            "pixels_differing_from_main": ndiff,
+            "rmse_vs_main": float(d2.pow(2).mean().sqrt()),
+            "note": "brute force and the reference BVH traversal agree except on exact distance ties"}
+        scene.set_traversal(args.traversal)
+        scene.set_variant(args.variant)
     if world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
         gpu_np = img.cpu().numpy() if img is not None else None
         res, parity = cpu_baseline(sd, spec, u, gpu_np, threads)
         out["cpu_baseline"] = {"value": round(res["bvh"]["value"], 4), "unit": "Msamples/s", "cores": threads,
                                "kind": "port",
-                               "sample": f"pixels i = {res['bvh']['stride'] // 2} + {res['bvh']['stride']}k in raster "
-                                         f"order ({res['bvh']['pixels']} of {spec.width * spec.height}), full spp, "
-                                         f"reference BVH traversal (compute.glsl:410-460), "
+                               "sample": f"{res['bvh']['pixels']} of {spec.width * spec.height} pixels, "
+                                         f"i = floor(k*{spec.width * spec.height}/{res['bvh']['pixels']}) in raster "
+                                         f"order, full spp, reference BVH traversal (compute.glsl:410-460), "
                                          f"{res['bvh']['seconds']:.1f} s",
                                "brute_force": {"value": round(res["brute"]["value"], 4),
                                                "pixels": res["brute"]["pixels"],
