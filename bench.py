@@ -36,6 +36,7 @@ METRIC = "Msamples/sec at 1920×1080 Cornell+OBJ; per-pixel RMSE vs CPU ref"
 VALU_PEAK_TFLOPS = 157.3   # MI355X FP32 vector peak (MI355X_MICROARCH.md, chip-level parameters)
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec
 FLOP_PER_TEST = 53
+FLOP_PER_VISIT = 24        # BVH interior node: 2 boxes x (6 sub + 6 div), compute.glsl:382-408
 BYTES_PER_TEST = 36        # a, b, c positions
 KERNEL_NAMES = {"brute": "render_smem (rt2_render.hip, variant smem/256/masked8/coop32)",
                 "bvh": "render_bvh3 (rt2_render.hip, variant bvh3/256/t16)"}
@@ -169,21 +170,23 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     st = scene.stats(reset=True)
-    t = torch.tensor([elapsed, kern_ms, float(st.tests), float(st.segments)], dtype=torch.float64, device="cuda")
+    t = torch.tensor([elapsed, kern_ms, float(st.tests), float(st.segments), float(st.node_visits)],
+                     dtype=torch.float64, device="cuda")
     if world > 1:
         tmax = t.clone()
         dist.all_reduce(tmax[:2], op=dist.ReduceOp.MAX)
         tsum = t.clone()
         dist.all_reduce(tsum[2:], op=dist.ReduceOp.SUM)
         elapsed, kern_ms = float(tmax[0]), float(tmax[1])
-        tests, segs = float(tsum[2]), float(tsum[3])
+        tests, segs, visits = float(tsum[2]), float(tsum[3]), float(tsum[4])
     else:
-        tests, segs = float(st.tests), float(st.segments)
+        tests, segs, visits = float(st.tests), float(st.segments), float(st.node_visits)
 
     samples_per_step = spec.width * spec.height * spec.rays * spec.frames
     value = samples_per_step * args.steps / elapsed / 1e6
     tests_per_launch = tests / args.steps / world
-    flops = FLOP_PER_TEST * tests_per_launch / (kern_ms * 1e-3) / 1e12
+    visits_per_launch = visits / args.steps / world
+    flops = (FLOP_PER_TEST * tests_per_launch + FLOP_PER_VISIT * visits_per_launch) / (kern_ms * 1e-3) / 1e12
     hbm_read = BYTES_PER_TEST * tests_per_launch / (kern_ms * 1e-3) / 1e9
 
     if rank != 0:
@@ -214,6 +217,8 @@ def main():
                      "frac": round(flops / VALU_PEAK_TFLOPS, 4), "traffic": None,
                      "kernel": KERNEL_NAMES[args.traversal], "kernel_ms": round(kern_ms, 3),
                      "tests_per_launch": int(tests_per_launch),
+                     "node_visits_per_launch": int(visits_per_launch),
+                     "flop_model": "53 x ray-triangle tests + 24 x BVH interior visits (2 slab boxes)",
                      "segments_per_sample": round(segs / (samples_per_step * args.steps), 4),
                      "hbm_read_algorithmic": {"achieved": round(hbm_read, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                               "frac": round(hbm_read / HBM_PEAK_GBS, 3),
@@ -258,6 +263,9 @@ def main():
             "kernel_ms": round(float(np.mean([a.elapsed_time(b) for a, b in ev2])), 3),
             "segments_per_sample": round(st2.segments / (samples_per_step * args.steps), 4),
             "tests_per_segment": round(st2.tests / max(st2.segments, 1), 3),
+            "node_visits_per_segment": round(st2.node_visits / max(st2.segments, 1), 3),
+            "valu_tflops": round((FLOP_PER_TEST * st2.tests + FLOP_PER_VISIT * st2.node_visits) / args.steps
+                                 / (float(np.mean([a.elapsed_time(b) for a, b in ev2])) * 1e-3) / 1e12, 3),
             "pixels_differing_from_main": ndiff,
             "rmse_vs_main": float(d2.pow(2).mean().sqrt()),
             "note": "brute force and the reference BVH traversal agree except on exact distance ties"}

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define RT2_ABI_VERSION 1
+#define RT2_ABI_VERSION 2
 
 /* Material types: mesh.h:16-22 == compute.glsl:7-13 */
 enum {
@@ -124,7 +124,10 @@ typedef struct rt2_shard {
 typedef struct rt2_stats {
     uint64_t samples;   /* pixel-rays traced = pixels * R * F              */
     uint64_t segments;  /* closest-hit queries (bounces actually traced)     */
-    uint64_t tests;     /* ray-triangle tests = segments * N (brute force)   */
+    uint64_t tests;     /* ray-triangle tests = segments * N (brute force);
+                           leaf tests (BVH traversal)                        */
+    uint64_t node_visits; /* BVH traversal: interior nodes popped (box pairs
+                             tested); 0 for brute force                      */
 } rt2_stats;
 
 const char* rt2_last_error(void);

@@ -2052,6 +2052,7 @@ extern "C" int rt2_scene_stats(rt2_scene* s, rt2_stats* out, int reset) {
     // brute force tests every triangle per segment; the BVH kernel counts its
     // leaf tests in c[2]
     out->tests = s->last_kind == 3 ? c[2] : c[1] * (unsigned long long)s->n_tris;
+    out->node_visits = s->last_kind == 3 ? c[3] : 0;
     if (reset) {
         s->samples = 0;
         HIPCHECK(hipMemset(s->d_counters, 0, sizeof(c)));

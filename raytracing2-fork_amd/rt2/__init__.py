@@ -111,8 +111,12 @@ class Shard(C.Structure):
     _fields_ = [("tile_rows", C.c_int32), ("rank", C.c_int32), ("nranks", C.c_int32)]
 
 
+ABI_VERSION = 2  # include/rt2.h RT2_ABI_VERSION
+
+
 class Stats(C.Structure):
-    _fields_ = [("samples", C.c_uint64), ("segments", C.c_uint64), ("tests", C.c_uint64)]
+    _fields_ = [("samples", C.c_uint64), ("segments", C.c_uint64), ("tests", C.c_uint64),
+                ("node_visits", C.c_uint64)]
 
 
 class CameraDesc(C.Structure):
@@ -236,6 +240,8 @@ def lib() -> C.CDLL:
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
+    if L.rt2_abi_version() != ABI_VERSION:
+        raise RT2Error(f"librt2.so ABI {L.rt2_abi_version()} != {ABI_VERSION}: rebuild (make -C raytracing2-fork_amd)")
     _lib = L
     return L
 
