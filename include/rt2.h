@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define RT2_ABI_VERSION 2
+#define RT2_ABI_VERSION 3
 
 /* Material types: mesh.h:16-22 == compute.glsl:7-13 */
 enum {
@@ -130,6 +130,15 @@ typedef struct rt2_stats {
                              tested); 0 for brute force                      */
 } rt2_stats;
 
+/* An 8-bit image as stb_image returns it: `channels` (1..4) interleaved
+ * bytes per pixel, rows of width*channels bytes, row 0 first in memory. */
+typedef struct rt2_image {
+    int32_t width;
+    int32_t height;
+    int32_t channels;
+    uint8_t* pixels;
+} rt2_image;
+
 const char* rt2_last_error(void);
 int rt2_abi_version(void);
 
@@ -216,6 +225,18 @@ int rt2_scene_set_traversal(rt2_scene* scene, int traversal);
  * frame_count * pixels * 16 B of device scratch per scene. */
 int rt2_scene_set_frame_split(rt2_scene* scene, int enable);
 
+/* Replaces binding the loader's textures to units 0..4 (rayTracing.cpp:
+ * 1315-1320; Texture2D(path), textureClass.cpp:55-104): the images are copied
+ * to HBM as RGBA8 with GL's unpack of GL_RED/GL_RG/GL_RGB/GL_RGBA bytes
+ * (4-byte row alignment, GL_UNPACK_ALIGNMENT's default) and the 1-channel
+ * swizzle (r, r, r, 1).  TEXTURE materials then sample texture
+ * `textureIndex` with GL_LINEAR + GL_REPEAT (getTriangleTextureColor,
+ * compute.glsl:342-368): black when textureIndex is outside [0,
+ * uniforms->numTextures), magenta for an index >= 5 (the shader binds five
+ * samplers), black for an index with no image here (an unbound unit).
+ * n = 0 removes the textures. */
+int rt2_scene_set_textures(rt2_scene* scene, const rt2_image* images, int32_t n);
+
 /* ------------------------------------------------------------------------
  * (2) Host surface
  * ---------------------------------------------------------------------- */
@@ -228,8 +249,19 @@ rt2_scene_data* rt2_sd_create(void);
 void rt2_sd_destroy(rt2_scene_data* sd);
 
 /* getTrianglesData_ (mesh.h:279-613): first *.obj of the folder, every *.mtl
- * of the folder, texture names from <folder>/textures. Appends. */
+ * of the folder, every file of <folder>/textures decoded as a texture (in
+ * directory order, flipped vertically on load, like Texture2D(path)).
+ * Appends. */
 int rt2_sd_load_obj_folder(rt2_scene_data* sd, const char* folder);
+/* Decoded texture i of the scene data (pixels owned by sd) or < 0. */
+int rt2_sd_texture(const rt2_scene_data* sd, int32_t i, rt2_image* out_view);
+
+/* stbi_set_flip_vertically_on_load(flip); stbi_load(path, &w, &h, &n, 0)
+ * (external/stb/stb_image.h v2.30 as Texture2D uses it), restated: PNG (all
+ * depths/colour types, tRNS, interlace) and sequential-Huffman JPEG.  The
+ * pixels are malloc'ed; release them with rt2_image_free. */
+int rt2_image_load(const char* path, int32_t flip_vertically, rt2_image* out);
+void rt2_image_free(rt2_image* image);
 /* Appends one material; returns its index or < 0. */
 int32_t rt2_sd_add_material(rt2_scene_data* sd, const rt2_material* m);
 /* Appends one triangle (and its BVH triangle) as a builder would. */

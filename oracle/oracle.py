@@ -35,6 +35,8 @@ def lib() -> C.CDLL:
         L.oracle_render_pixels.restype = C.c_int
         L.oracle_render_pixels.argtypes = [P, C.c_int32, P, C.c_int32, P, C.c_int32, P, C.c_uint32, C.c_uint32, P,
                                            C.c_int64, C.c_int32, C.c_int32, P, P, P, P]
+        L.oracle_set_textures.restype = C.c_int
+        L.oracle_set_textures.argtypes = [P, P, C.c_int32]
         L.oracle_pcg_next.restype = C.c_uint32
         L.oracle_pcg_next.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_float)]
         L.oracle_ray_triangle.restype = C.c_int
@@ -99,6 +101,23 @@ def render_pixels(triangles: np.ndarray, materials: np.ndarray, uniforms, xs, ys
     if rc != 0:
         raise RuntimeError(f"oracle_render_pixels failed: {rc}")
     return acc, acc8, segs.value, tests.value
+
+
+_tex_keep = None
+
+
+def set_textures(images) -> None:
+    """images: list of uint8 arrays shaped (h, w, channels) in stb layout
+    (row 0 first in memory).  Held by the library until the next call."""
+    global _tex_keep
+    arrs = [np.ascontiguousarray(a, dtype=np.uint8) for a in images]
+    whn = np.array([[a.shape[1], a.shape[0], a.shape[2] if a.ndim == 3 else 1] for a in arrs],
+                   dtype=np.int32).reshape(-1)
+    ptrs = (C.c_void_p * max(len(arrs), 1))(*[a.ctypes.data for a in arrs])
+    _tex_keep = (arrs, whn, ptrs)
+    rc = lib().oracle_set_textures(whn.ctypes.data if len(arrs) else None, C.addressof(ptrs), len(arrs))
+    if rc != 0:
+        raise RuntimeError("oracle_set_textures failed")
 
 
 def pcg_sequence(seed: int, n: int):

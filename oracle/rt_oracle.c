@@ -254,6 +254,107 @@ static hit_t closest(const ctx_t* c, v3 o, v3 d, uint64_t* tests) {
     return r;
 }
 
+/* ---- textures (getTriangleTextureColor, compute.glsl:342-368) ------------
+ * Set by oracle_set_textures from stb-layout images (w, h, n, bytes); held as
+ * RGBA8 after GL's unpack (GL_UNPACK_ALIGNMENT 4: rows every align4(w*n)
+ * bytes, bytes past the buffer read as 0) and Texture2D's swizzles
+ * (textureClass.cpp:70-90: 1 channel -> r,r,r,1; GL_RG -> r,g,0,1). */
+typedef struct {
+    int32_t w, h;
+    uint8_t* rgba;
+} otex_t;
+static otex_t g_tex[64];
+static int32_t g_ntex = 0;
+
+int oracle_set_textures(const int32_t* whn, const uint8_t* const* pixels, int32_t n) {
+    for (int i = 0; i < g_ntex; i++) free(g_tex[i].rgba);
+    g_ntex = 0;
+    if (n < 0 || n > 64) return -1;
+    for (int i = 0; i < n; i++) {
+        const int32_t w = whn[3 * i], h = whn[3 * i + 1], ch = whn[3 * i + 2];
+        if (w < 1 || h < 1 || ch < 1 || ch > 4) return -1;
+        const size_t stride = ((size_t)w * ch + 3) & ~(size_t)3, total = (size_t)w * h * ch;
+        uint8_t* q = (uint8_t*)malloc((size_t)w * h * 4);
+        for (int y = 0; y < h; y++)
+            for (int x = 0; x < w; x++) {
+                uint8_t c[4] = {0, 0, 0, 255};
+                for (int k = 0; k < ch; k++) {
+                    const size_t at = (size_t)y * stride + (size_t)x * ch + k;
+                    c[k] = at < total ? pixels[i][at] : 0;
+                }
+                uint8_t* o = q + ((size_t)y * w + x) * 4;
+                if (ch == 1) {
+                    o[0] = o[1] = o[2] = c[0];
+                    o[3] = 255;
+                } else if (ch == 2) {
+                    o[0] = c[0];
+                    o[1] = c[1];
+                    o[2] = 0;
+                    o[3] = 255;
+                } else {
+                    o[0] = c[0];
+                    o[1] = c[1];
+                    o[2] = c[2];
+                    o[3] = ch == 4 ? c[3] : 255;
+                }
+            }
+        g_tex[i].w = w;
+        g_tex[i].h = h;
+        g_tex[i].rgba = q;
+        g_ntex = i + 1;
+    }
+    return 0;
+}
+
+static int tex_wrap(float f, int n) {
+    const int i = (f >= -1073741824.0f && f <= 1073741824.0f) ? (int)f : 0;
+    const int r = i % n;
+    return r < 0 ? r + n : r;
+}
+
+/* texture(sampler2D, uv): GL_LINEAR (no mipmaps) + GL_REPEAT, GL 4.3 §8.14.2,
+ * unorm8 texels c/255, evaluated in binary32 as written. */
+static v3 tex_sample(const otex_t* t, float s, float tc) {
+    const float u = s * (float)t->w - 0.5f;
+    const float v = tc * (float)t->h - 0.5f;
+    const float fu = floorf(u), fv = floorf(v);
+    const float a = u - fu, b = v - fv;
+    const int i0 = tex_wrap(fu, t->w), j0 = tex_wrap(fv, t->h);
+    const int i1 = i0 + 1 == t->w ? 0 : i0 + 1, j1 = j0 + 1 == t->h ? 0 : j0 + 1;
+    const uint8_t* T00 = t->rgba + ((size_t)j0 * t->w + i0) * 4;
+    const uint8_t* T10 = t->rgba + ((size_t)j0 * t->w + i1) * 4;
+    const uint8_t* T01 = t->rgba + ((size_t)j1 * t->w + i0) * 4;
+    const uint8_t* T11 = t->rgba + ((size_t)j1 * t->w + i1) * 4;
+    const float w00 = (1.0f - a) * (1.0f - b), w10 = a * (1.0f - b), w01 = (1.0f - a) * b, w11 = a * b;
+    float r[3];
+    for (int k = 0; k < 3; k++)
+        r[k] = w00 * ((float)T00[k] / 255.0f) + w10 * ((float)T10[k] / 255.0f) + w01 * ((float)T01[k] / 255.0f) +
+               w11 * ((float)T11[k] / 255.0f);
+    return mk(r[0], r[1], r[2]);
+}
+
+/* getTriangleTextureColor at the closest hit of (o, d) on triangle t: the
+ * barycentrics of rayTriangleIntersect (:307-338, w = 1 - u - v),
+ * uv = aTex*u + bTex*v + cTex*w. */
+static v3 texture_color(const ctx_t* c, int tex_index, const oracle_triangle* t, v3 o, v3 d) {
+    if (tex_index < 0 || tex_index >= c->u->numTextures) return mk(0.0f, 0.0f, 0.0f);
+    if (tex_index > 4) return mk(1.0f, 0.0f, 1.0f);
+    if (tex_index >= g_ntex) return mk(0.0f, 0.0f, 0.0f);
+    v3 a = v4xyz(t->a), b = v4xyz(t->b), cc = v4xyz(t->c);
+    v3 e0 = sub(b, a), e1 = sub(cc, a);
+    v3 cross01 = cross(e0, e1);
+    float det = -dot(d, cross01);
+    float invDet = 1.0f / det;
+    v3 ao = sub(o, a);
+    v3 q = cross(d, ao);
+    float u = -dot(e1, q) * invDet;
+    float v = dot(e0, q) * invDet;
+    float w = 1.0f - u - v;
+    float s = t->aTex[0] * u + t->bTex[0] * v + t->cTex[0] * w;
+    float tc = t->aTex[1] * u + t->bTex[1] * v + t->cTex[1] * w;
+    return tex_sample(&g_tex[tex_index], s, tc);
+}
+
 /* trace, compute.glsl:472-563 */
 static v3 trace(const ctx_t* c, v3 origin, v3 dir, uint32_t* rng, uint64_t* segs, uint64_t* tests) {
     v3 rayColor = mk(1.0f, 1.0f, 1.0f);
@@ -272,6 +373,8 @@ static v3 trace(const ctx_t* c, v3 origin, v3 dir, uint32_t* rng, uint64_t* segs
             v3 hitPoint = add(origin, muls(dir, h.dst));
             int mi = t->materialIndex;
             const oracle_material* m = &c->mats[mi];
+            v3 tex = m->materialType == TEXTURE ? texture_color(c, m->textureIndex, t, origin, dir)
+                                                : mk(0.0f, 0.0f, 0.0f);
             if (m->materialType != GLASS)
                 origin = sub(hitPoint, muls(muls(dir, h.dst), -1e-3f));
             else
@@ -282,9 +385,7 @@ static v3 trace(const ctx_t* c, v3 origin, v3 dir, uint32_t* rng, uint64_t* segs
             case DIFFUSE:
             case TEXTURE:
                 dir = normalize(add(normal, rnd_dir(rng)));
-                /* TEXTURE with no bound textures: getTriangleTextureColor
-                 * returns black (compute.glsl:349-350). */
-                attenuation = m->materialType == DIFFUSE ? v4xyz(m->color) : mk(0.0f, 0.0f, 0.0f);
+                attenuation = m->materialType == DIFFUSE ? v4xyz(m->color) : tex;
                 break;
             case SPECULAR: {
                 v3 diffuseDirection = normalize(add(normal, rnd_dir(rng)));
@@ -346,7 +447,7 @@ static inline v3 normalize_color(v3 c) {
 
 /* traceBasic, compute.glsl:565-645 — the interactive one-ray preview.  `Ray
  * ray;` leaves insideGlass uninitialised in the shader (:674); it starts false
- * here.  TEXTURE samples nothing (no textures bound), as in trace(). */
+ * here. */
 static v3 trace_basic(const ctx_t* c, v3 origin, v3 dir, uint64_t* segs, uint64_t* tests) {
     v3 colorCumulative = mk(0.0f, 0.0f, 0.0f);
     int insideGlass = 0;
@@ -360,8 +461,10 @@ static v3 trace_basic(const ctx_t* c, v3 origin, v3 dir, uint64_t* segs, uint64_
             v3 a = v4xyz(t->a), b = v4xyz(t->b), cc = v4xyz(t->c);
             v3 normal = normalize(cross(sub(b, a), sub(cc, a)));
             v3 hitPoint = add(origin, muls(dir, h.dst));
-            origin = sub(hitPoint, muls(normal, 1e-4f));
             const oracle_material* m = &c->mats[t->materialIndex];
+            v3 tex = m->materialType == TEXTURE ? texture_color(c, m->textureIndex, t, origin, dir)
+                                                : mk(0.0f, 0.0f, 0.0f);
+            origin = sub(hitPoint, muls(normal, 1e-4f));
             switch (m->materialType) {
             case SPECULAR:
                 colorCumulative = add(colorCumulative, v4xyz(m->color));
@@ -372,7 +475,7 @@ static v3 trace_basic(const ctx_t* c, v3 origin, v3 dir, uint64_t* segs, uint64_
             case CHECKER: {
                 v3 color;
                 if (m->materialType == TEXTURE) {
-                    color = mk(0.0f, 0.0f, 0.0f);
+                    color = tex;
                 } else if (m->materialType == DIFFUSE) {
                     color = v4xyz(m->color);
                 } else {

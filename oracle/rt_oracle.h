@@ -64,6 +64,10 @@ int oracle_render_pixels(const oracle_triangle* tris, int32_t n_tris, const orac
                          uint32_t frame_count, const int32_t* px, int64_t n_px, int32_t mode, int32_t threads,
                          float* out_accum, uint32_t* out_acc8, uint64_t* out_segments, uint64_t* out_tests);
 
+/* Textures for TEXTURE materials (global to the library): n stb-layout
+ * images, whn = (width, height, channels) triples.  n = 0 clears. */
+int oracle_set_textures(const int32_t* whn, const uint8_t* const* pixels, int32_t n);
+
 uint32_t oracle_pcg_next(uint32_t* state, float* out);
 int oracle_ray_triangle(const float o[3], const float d[3], const oracle_triangle* t, float* dst);
 void oracle_sky(const float d[3], float out[3]);

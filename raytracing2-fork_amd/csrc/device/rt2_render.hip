@@ -65,6 +65,11 @@ struct RenderParams {
     const float4* bvh_recs; // BVH v2: child-pair records (4 float4 each)
     int bvh_root;           // BVH v2: stack entry of node 0
     int recs_ok;            // BVH v3: every record coordinate in {0} U [2^-37, 2^59]
+    const rt2_triangle* raw;     // as uploaded (texture coordinates)
+    const uchar4* texels;        // all textures, RGBA8 after GL unpack + swizzle
+    const int4* tex_desc;        // per texture {width, height, offset lo, offset hi}
+    int n_tex;                   // textures uploaded
+    int num_textures;            // uniforms.numTextures
 };
 
 enum : int { ST_NEED_ITEM = 0, ST_NEW_FRAME = 1, ST_NEW_RAY = 2, ST_TRACE = 3, ST_DONE = 4 };
@@ -458,8 +463,10 @@ __device__ __forceinline__ void advance(Lane& L, const RenderParams& p) {
                 if (it < p.n_items) {
                     // frame_split: item = frame * n_pix + pixel (frame-major), so the
                     // last items of a launch are single pixel-frames
-                    const uint32_t f = p.frame_split ? (uint32_t)(it / p.n_pix) : 0u;
-                    L.item = (uint32_t)(it - (unsigned long long)f * p.n_pix);
+                    // n_items < 2^32 (checked on the host): 32-bit arithmetic
+                    const uint32_t it32 = (uint32_t)it, np32 = (uint32_t)p.n_pix;
+                    const uint32_t f = p.frame_split ? it32 / np32 : 0u;
+                    L.item = it32 - f * np32;
                     int lr = (int)(L.item / (uint32_t)p.W);
                     L.x = (int)(L.item - (uint32_t)lr * (uint32_t)p.W);
                     L.y = shard_row(lr, p.tile_rows, p.rank, p.nranks);
@@ -532,13 +539,67 @@ __device__ __forceinline__ void end_path(Lane& L, const RenderParams& p) {
     L.st = L.frame < p.frame_count ? ST_NEW_FRAME : ST_NEED_ITEM;
 }
 
+// texture(sampler2D, uv) with GL_LINEAR (no mipmaps) + GL_REPEAT, GL 4.3
+// §8.14.2: u = s*w - 1/2, i0 = wrap(floor(u)), alpha = frac(u) (likewise v),
+// tau = (1-a)(1-b) T00 + a(1-b) T10 + (1-a)b T01 + ab T11 with unorm8
+// texels c/255.  Pinned in binary32, evaluated as written (oracle: same).
+__device__ __forceinline__ int tex_wrap(float f, int n) {
+    const int i = (f >= -1073741824.0f && f <= 1073741824.0f) ? (int)f : 0;  // NaN / huge -> 0
+    const int r = i % n;
+    return r < 0 ? r + n : r;
+}
+__device__ __forceinline__ f3 tex_sample(const RenderParams& p, int t, float s, float tc) {
+    const int4 dsc = p.tex_desc[t];
+    const int w = dsc.x, h = dsc.y;
+    const unsigned long long off = (unsigned long long)(uint32_t)dsc.z | (unsigned long long)(uint32_t)dsc.w << 32;
+    const float u = s * (float)w - 0.5f;
+    const float v = tc * (float)h - 0.5f;
+    const float fu = floorf(u), fv = floorf(v);
+    const float a = u - fu, b = v - fv;
+    const int i0 = tex_wrap(fu, w), j0 = tex_wrap(fv, h);
+    const int i1 = i0 + 1 == w ? 0 : i0 + 1, j1 = j0 + 1 == h ? 0 : j0 + 1;
+    const uchar4* T = p.texels + off;
+    const uchar4 t00 = T[(size_t)j0 * w + i0], t10 = T[(size_t)j0 * w + i1];
+    const uchar4 t01 = T[(size_t)j1 * w + i0], t11 = T[(size_t)j1 * w + i1];
+    const float w00 = (1.0f - a) * (1.0f - b), w10 = a * (1.0f - b), w01 = (1.0f - a) * b, w11 = a * b;
+#define RT2_TEXCH(c) \
+    (w00 * ((float)t00.c / 255.0f) + w10 * ((float)t10.c / 255.0f) + w01 * ((float)t01.c / 255.0f) + \
+     w11 * ((float)t11.c / 255.0f))
+    return mk(RT2_TEXCH(x), RT2_TEXCH(y), RT2_TEXCH(z));
+#undef RT2_TEXCH
+}
+
+// getTriangleTextureColor (compute.glsl:342-368) at the closest hit of ray
+// (o, d) on triangle bi: barycentrics recomputed with the test's own
+// arithmetic (rayTriangleIntersect :322-338, w = 1 - u - v), uv = aTex*u +
+// bTex*v + cTex*w.
+__device__ __forceinline__ f3 texture_color(const RenderParams& p, int tex_index, int bi, const f3& o, const f3& d) {
+    if (tex_index < 0 || tex_index >= p.num_textures) return mk(0.0f, 0.0f, 0.0f);
+    if (tex_index > 4) return mk(1.0f, 0.0f, 1.0f);
+    if (tex_index >= p.n_tex) return mk(0.0f, 0.0f, 0.0f);  // unit with no texture bound
+    const MtQ q = mt_quantities(o, d, p.tri[3 * bi], p.tri[3 * bi + 1], p.tri[3 * bi + 2]);
+    const float inv = 1.0f / q.det;
+    const float u = -q.U * inv;
+    const float v = q.V * inv;
+    const float w = 1.0f - u - v;
+    const rt2_triangle& t = p.raw[bi];
+    const float s = t.aTex.x * u + t.bTex.x * v + t.cTex.x * w;
+    const float tc = t.aTex.y * u + t.bTex.y * v + t.cTex.y * w;
+    return tex_sample(p, tex_index, s, tc);
+}
+
 // Phase C: scatter at the closest hit (compute.glsl:485-559).
 __device__ __forceinline__ void shade(Lane& L, const RenderParams& p, float best, int bi) {
     if (bi >= 0) {
+        const int mi = p.tri_mtl[bi];
+        // the texture lookup first, while little else is live (it needs the
+        // segment's own origin, which the scatter below overwrites)
+        f3 tex = mk(0.0f, 0.0f, 0.0f);
+        if (p.mats[mi].materialType == RT2_TEXTURE) tex = texture_color(p, p.mats[mi].textureIndex, bi, L.o, L.d);
         const float4 t2 = p.tri[3 * bi + 2];
         const f3 normal = normalize(mk(t2.y, t2.z, t2.w));  // normalize(cross01), compute.glsl:331
         const f3 hitPoint = add(L.o, muls(L.d, best));      // compute.glsl:330
-        const rt2_material m = p.mats[p.tri_mtl[bi]];
+        const rt2_material m = p.mats[mi];
         if (m.materialType != RT2_GLASS)
             L.o = sub(hitPoint, muls(muls(L.d, best), -1e-3f));
         else
@@ -549,7 +610,7 @@ __device__ __forceinline__ void shade(Lane& L, const RenderParams& p, float best
         case RT2_DIFFUSE:
         case RT2_TEXTURE:
             L.d = normalize(add(normal, rnd_dir(L.seed)));
-            atten = m.materialType == RT2_DIFFUSE ? xyz4(m.color) : mk(0.0f, 0.0f, 0.0f);
+            atten = m.materialType == RT2_DIFFUSE ? xyz4(m.color) : tex;
             break;
         case RT2_SPECULAR: {
             f3 diffuseDir = normalize(add(normal, rnd_dir(L.seed)));
@@ -729,8 +790,8 @@ __global__ __launch_bounds__(BLOCK) void render_tiled(RenderParams p) {
 // COOP > 0: drain mode — once the item pool is exhausted (some lane is DONE)
 // and at most COOP lanes of the wave still trace, each live ray's closest hit
 // is computed by the whole wave (coop_closest), one ray at a time.
-template <int BLOCK, int G, int COOP>
-__global__ __launch_bounds__(BLOCK) void render_smem(RenderParams p) {
+template <int BLOCK, int G, int COOP, int WPE>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void render_smem(RenderParams p) {
     cfloat* tri = (cfloat*)p.tri;
     Lane L;
     lane_init(L);
@@ -1211,8 +1272,8 @@ __device__ __forceinline__ void bvh_leaf3(TravState3& T, int e, const rt2_node* 
     }
 }
 
-template <int BLOCK, int THRESH, int DIV>
-__global__ __launch_bounds__(BLOCK) void render_bvh3(RenderParams p) {
+template <int BLOCK, int THRESH, int DIV, int WPE>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void render_bvh3(RenderParams p) {
     extern __shared__ int bvh_stack[];
     int* st = bvh_stack + threadIdx.x;
     const float4* __restrict__ recs = p.bvh_recs;
@@ -1345,6 +1406,9 @@ __device__ __forceinline__ f3 trace_basic(const RenderParams& p, f3 o, f3 d, int
         const float4 t2 = p.tri[3 * bi + 2];
         const f3 normal = normalize(mk(t2.y, t2.z, t2.w));
         const f3 hitPoint = add(o, muls(d, best));
+        const rt2_material mm = p.mats[p.tri_mtl[bi]];
+        const f3 tex = mm.materialType == RT2_TEXTURE ? texture_color(p, mm.textureIndex, bi, o, d)
+                                                      : mk(0.0f, 0.0f, 0.0f);
         o = sub(hitPoint, muls(normal, 1e-4f));  // :579
         const rt2_material m = p.mats[p.tri_mtl[bi]];
         switch (m.materialType) {
@@ -1357,7 +1421,7 @@ __device__ __forceinline__ f3 trace_basic(const RenderParams& p, f3 o, f3 d, int
         case RT2_CHECKER: {
             f3 color;
             if (m.materialType == RT2_TEXTURE) {
-                color = mk(0.0f, 0.0f, 0.0f);  // no textures bound: black, as in trace()
+                color = tex;
             } else if (m.materialType == RT2_DIFFUSE) {
                 color = xyz4(m.color);
             } else {
@@ -1551,6 +1615,9 @@ struct rt2_scene {
     rt2_node* d_nodes = nullptr;
     float4* d_recs = nullptr;                   // BVH v2 child-pair records
     float4* d_fb = nullptr;                     // frame_split scratch (per-frame colours)
+    uchar4* d_texels = nullptr;                 // textures, RGBA8
+    int4* d_tex_desc = nullptr;
+    int n_tex = 0;
     size_t fb_bytes = 0;
     int bvh_root = 0;                           // BVH v2 stack entry of node 0
     int recs_ok = 0;                            // BVH v3 fast-path precondition on the boxes
@@ -1650,6 +1717,65 @@ static int bvh_records(const rt2_node* nodes, int n_nodes, std::vector<float4>& 
     }
     root = enc(0);
     return n_int;
+}
+
+// GL's unpack of a tightly packed stb image (GL_UNPACK_ALIGNMENT 4: rows
+// start every align4(w*n) bytes; bytes past the buffer read as 0 — the
+// reference reads past its allocation there) into RGBA8, with the swizzles of
+// Texture2D(path) (1 channel: r,r,r,1; GL_RG: r,g,0,1; GL_RGB: r,g,b,1).
+static void gl_unpack_rgba8(const rt2_image& im, uchar4* out) {
+    const size_t n = (size_t)im.channels, stride = ((size_t)im.width * n + 3) & ~(size_t)3;
+    const size_t total = (size_t)im.width * im.height * n;
+    auto at = [&](size_t i) -> uint8_t { return i < total ? im.pixels[i] : (uint8_t)0; };
+    for (int j = 0; j < im.height; j++)
+        for (int i = 0; i < im.width; i++) {
+            const size_t b = (size_t)j * stride + (size_t)i * n;
+            uchar4 t;
+            if (n == 1) t = make_uchar4(at(b), at(b), at(b), 255);
+            else if (n == 2) t = make_uchar4(at(b), at(b + 1), 0, 255);
+            else if (n == 3) t = make_uchar4(at(b), at(b + 1), at(b + 2), 255);
+            else t = make_uchar4(at(b), at(b + 1), at(b + 2), at(b + 3));
+            out[(size_t)j * im.width + i] = t;
+        }
+}
+
+extern "C" int rt2_scene_set_textures(rt2_scene* s, const rt2_image* images, int32_t n) {
+    if (!s || n < 0 || (n > 0 && !images)) {
+        rt2h::set_error("rt2_scene_set_textures: bad argument");
+        return -1;
+    }
+    size_t total = 0;
+    for (int i = 0; i < n; i++) {
+        const rt2_image& im = images[i];
+        if (im.width < 1 || im.height < 1 || im.channels < 1 || im.channels > 4 || !im.pixels) {
+            rt2h::set_error("rt2_scene_set_textures: image " + std::to_string(i) + " is empty or has " +
+                            std::to_string(im.channels) + " channels");
+            return -1;
+        }
+        total += (size_t)im.width * im.height;
+    }
+    HIPCHECK(hipSetDevice(s->device));
+    HIPCHECK(hipDeviceSynchronize());
+    (void)hipFree(s->d_texels);
+    (void)hipFree(s->d_tex_desc);
+    s->d_texels = nullptr;
+    s->d_tex_desc = nullptr;
+    s->n_tex = 0;
+    if (n == 0) return 0;
+    std::vector<uchar4> host(total);
+    std::vector<int4> desc(n);
+    size_t off = 0;
+    for (int i = 0; i < n; i++) {
+        gl_unpack_rgba8(images[i], host.data() + off);
+        desc[i] = make_int4(images[i].width, images[i].height, (int)(uint32_t)(off & 0xffffffffu), (int)(off >> 32));
+        off += (size_t)images[i].width * images[i].height;
+    }
+    HIPCHECK(hipMalloc(&s->d_texels, total * sizeof(uchar4)));
+    HIPCHECK(hipMalloc(&s->d_tex_desc, n * sizeof(int4)));
+    HIPCHECK(hipMemcpy(s->d_texels, host.data(), total * sizeof(uchar4), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(s->d_tex_desc, desc.data(), n * sizeof(int4), hipMemcpyHostToDevice));
+    s->n_tex = n;
+    return 0;
 }
 
 extern "C" int rt2_scene_set_frame_split(rt2_scene* s, int enable) {
@@ -1759,6 +1885,8 @@ extern "C" void rt2_scene_destroy(rt2_scene* s) {
     (void)hipFree(s->d_nodes);
     (void)hipFree(s->d_recs);
     (void)hipFree(s->d_fb);
+    (void)hipFree(s->d_texels);
+    (void)hipFree(s->d_tex_desc);
     (void)hipFree(s->d_counters);
     delete s;
 }
@@ -1800,13 +1928,14 @@ hipError_t launch_t(const RenderParams& p, int blocks, size_t lds, hipStream_t s
     if constexpr (KIND == K_TILED)
         hipLaunchKernelGGL((render_tiled<BLOCK, MT, UNROLL>), dim3(blocks), dim3(BLOCK), lds, st, p);
     else if constexpr (KIND == K_SMEM)
-        hipLaunchKernelGGL((render_smem<BLOCK, MT % 1000, MT / 1000>), dim3(blocks), dim3(BLOCK), 0, st, p);
+        hipLaunchKernelGGL((render_smem<BLOCK, MT % 1000, MT / 1000, UNROLL>), dim3(blocks), dim3(BLOCK), 0, st, p);
     else if constexpr (KIND == K_BVH)
         hipLaunchKernelGGL((render_bvh<BLOCK>), dim3(blocks), dim3(BLOCK), lds, st, p);
     else if constexpr (KIND == K_BVH2)
         hipLaunchKernelGGL((render_bvh2<BLOCK, MT>), dim3(blocks), dim3(BLOCK), lds, st, p);
     else if constexpr (KIND == K_BVH3)
-        hipLaunchKernelGGL((render_bvh3<BLOCK, MT % 1000, MT / 1000>), dim3(blocks), dim3(BLOCK), lds, st, p);
+        hipLaunchKernelGGL((render_bvh3<BLOCK, MT % 1000, MT / 1000, UNROLL>), dim3(blocks), dim3(BLOCK), lds, st,
+                           p);
     else
         hipLaunchKernelGGL((render_resident<BLOCK, MT, UNROLL>), dim3(blocks), dim3(BLOCK), lds, st, p);
     return hipGetLastError();
@@ -1816,13 +1945,14 @@ hipError_t occ_t(int* occ, size_t lds) {
     if constexpr (KIND == K_TILED)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_tiled<BLOCK, MT, UNROLL>, BLOCK, lds);
     else if constexpr (KIND == K_SMEM)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_smem<BLOCK, MT % 1000, MT / 1000>, BLOCK, 0);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_smem<BLOCK, MT % 1000, MT / 1000, UNROLL>,
+                                                            BLOCK, 0);
     else if constexpr (KIND == K_BVH)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_bvh<BLOCK>, BLOCK, lds);
     else if constexpr (KIND == K_BVH2)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_bvh2<BLOCK, MT>, BLOCK, lds);
     else if constexpr (KIND == K_BVH3)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_bvh3<BLOCK, MT % 1000, MT / 1000>, BLOCK,
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_bvh3<BLOCK, MT % 1000, MT / 1000, UNROLL>, BLOCK,
                                                             lds);
     else
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_resident<BLOCK, MT, UNROLL>, BLOCK, lds);
@@ -1882,11 +2012,14 @@ const Variant kVariants[] = {
     RT2_VARIANT(K_BVH3, 128, 16, 1, "bvh3/128/t16"),                 // 49
     RT2_VARIANT(K_BVH3, 256, 1016, 1, "bvh3/256/t16/div64"),         // 50
     RT2_VARIANT(K_BVH3, 256, 1008, 1, "bvh3/256/t8/div64"),          // 51
+    RT2_VARIANT(K_SMEM, 256, 32108, 6, "smem/256/masked8/coop32/w6"), // 52
+    RT2_VARIANT(K_BVH3, 256, 16, 5, "bvh3/256/t16/w5"),              // 53
+    RT2_VARIANT(K_BVH3, 256, 8, 5, "bvh3/256/t8/w5"),                // 54
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr size_t kResidentMaxBytes = 112 * 1024;
 constexpr int kSmemMaxTris = 16384;
-constexpr int kDefaultBvhVariant = 46;
+constexpr int kDefaultBvhVariant = 53;
 }  // namespace
 
 extern "C" const char* rt2_variant_name(int v) { return v >= 0 && v < kNumVariants ? kVariants[v].name : nullptr; }
@@ -1914,6 +2047,11 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     std::memset(&p, 0, sizeof(p));
     p.tri = s->d_tri;
     p.tri_mtl = s->d_mtl;
+    p.raw = s->d_raw;
+    p.texels = s->d_texels;
+    p.tex_desc = s->d_tex_desc;
+    p.n_tex = s->n_tex;
+    p.num_textures = u->numTextures;
     p.mats = s->d_mats;
     p.n_tris = s->n_tris;
     p.n_mats = s->n_mats;

@@ -73,11 +73,22 @@ struct Box {
     }
 };
 
+// A decoded 8-bit image (stb_image's stbi_load result layout: rows of w*n
+// bytes, no padding, row 0 = first row in memory).
+struct Image {
+    int w = 0, h = 0, n = 0;
+    std::vector<uint8_t> px;
+};
+// stbi_load(path, ..., 0) after stbi_set_flip_vertically_on_load(flip)
+// (image.cpp); throws std::runtime_error on unsupported/corrupt files.
+Image load_image(const std::string& path, bool flip);
+
 struct SceneData {
     std::vector<rt2_triangle> tris;
     std::vector<BvhTri> btris;
     std::vector<rt2_material> mats;
     std::vector<std::string> tex_names;
+    std::vector<Image> textures;  // decoded, flipped on load (textureClass.cpp:55-68)
     std::vector<rt2_node> nodes;
 
     void push(const rt2_triangle& t) {

@@ -3,8 +3,7 @@
 // because they decide the arrays the render path consumes:
 //   - the OBJ is the first *.obj of the folder in directory order (:223-253);
 //   - textures: the regular files of <folder>/textures in directory order give
-//     the texture indices (:305-318) — only the names are kept here (texture
-//     sampling is SURVEY.md §8f row 3);
+//     the texture indices (:305-318); each is decoded (image.cpp) and kept;
 //   - every folder file whose text after its FIRST '.' is "mtl" is parsed, in
 //     directory order; a folder file with no '.' is an error (:328-339);
 //   - material `index` = running count of `newmtl` over all MTL files (:369),
@@ -93,15 +92,17 @@ extern "C" int rt2_sd_load_obj_folder(rt2_scene_data* sd, const char* folder_c) 
         std::ifstream objs(obj);
         if (!objs.is_open()) throw std::runtime_error("cannot open " + obj.string());
 
-        // Textures (mesh.h:305-318): names only.
+        // Textures (mesh.h:305-318): every file of textures/, in directory
+        // order, decoded as Texture2D(path) does (textureClass.cpp:55-68:
+        // flipped on load; a file stb cannot load throws).  Indices restart at
+        // 0 for each folder, as the reference's per-call texture vector.
         std::map<std::string, int> tex_index;
         std::vector<std::string> tex = filenames_in(folder / "textures");
-        const int tex_base = (int)sd->tex_names.size();
         for (size_t i = 0; i < tex.size(); i++) {
             tex_index[tex[i]] = (int)i;
+            sd->textures.push_back(load_image((folder / "textures" / tex[i]).string(), true));
             sd->tex_names.push_back(tex[i]);
         }
-        (void)tex_base;
 
         // MTL libraries (mesh.h:321-453).
         std::map<std::string, std::map<std::string, rt2_material>> libs;

@@ -98,6 +98,19 @@ extern "C" int rt2_sd_add_triangles(rt2_scene_data* sd, const rt2_triangle* tris
 extern "C" int32_t rt2_sd_num_triangles(const rt2_scene_data* sd) { return sd ? (int32_t)sd->tris.size() : 0; }
 extern "C" int32_t rt2_sd_num_materials(const rt2_scene_data* sd) { return sd ? (int32_t)sd->mats.size() : 0; }
 extern "C" int32_t rt2_sd_num_nodes(const rt2_scene_data* sd) { return sd ? (int32_t)sd->nodes.size() : 0; }
+extern "C" int rt2_sd_texture(const rt2_scene_data* sd, int32_t i, rt2_image* out) {
+    if (!sd || !out || i < 0 || i >= (int32_t)sd->textures.size()) {
+        rt2h::set_error("rt2_sd_texture: bad argument");
+        return -1;
+    }
+    const rt2h::Image& im = sd->textures[i];
+    out->width = im.w;
+    out->height = im.h;
+    out->channels = im.n;
+    out->pixels = const_cast<uint8_t*>(im.px.data());
+    return 0;
+}
+
 extern "C" int32_t rt2_sd_num_textures(const rt2_scene_data* sd) { return sd ? (int32_t)sd->tex_names.size() : 0; }
 extern "C" const rt2_triangle* rt2_sd_triangles(const rt2_scene_data* sd) { return sd ? sd->tris.data() : nullptr; }
 extern "C" const rt2_material* rt2_sd_materials(const rt2_scene_data* sd) { return sd ? sd->mats.data() : nullptr; }

@@ -79,6 +79,13 @@ class Material(C.Structure):  # Material, mesh.h:26-103
         return m
 
     @staticmethod
+    def texture(index: int, col=(1.0, 1.0, 1.0)) -> "Material":  # map_Kd in an MTL, mesh.h:430-450
+        m = Material.diffuse(col)
+        m.materialType = 5
+        m.textureIndex = int(index)
+        return m
+
+    @staticmethod
     def checker(scale: float) -> "Material":  # makeChecker, mesh.h:79-83
         m = Material.default()
         lib().rt2_material_make_checker(C.byref(m), float(scale))
@@ -111,7 +118,12 @@ class Shard(C.Structure):
     _fields_ = [("tile_rows", C.c_int32), ("rank", C.c_int32), ("nranks", C.c_int32)]
 
 
-ABI_VERSION = 2  # include/rt2.h RT2_ABI_VERSION
+ABI_VERSION = 3  # include/rt2.h RT2_ABI_VERSION
+
+
+class Image(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("channels", C.c_int32),
+                ("pixels", C.POINTER(C.c_uint8))]
 
 
 class Stats(C.Structure):
@@ -151,7 +163,8 @@ EXPORTED = [
     "rt2_sd_triangles", "rt2_sd_materials", "rt2_sd_nodes", "rt2_sd_bvh_triangles", "rt2_sd_texture_name",
     "rt2_material_default", "rt2_material_make_diffuse", "rt2_material_make_light", "rt2_material_make_specular",
     "rt2_material_make_checker", "rt2_material_make_glass", "rt2_camera_default", "rt2_camera_uniforms",
-    "rt2_uniforms_offline", "rt2_write_png",
+    "rt2_uniforms_offline", "rt2_write_png", "rt2_image_load", "rt2_image_free", "rt2_sd_texture",
+    "rt2_scene_set_textures",
 ]
 
 _lib: Optional[C.CDLL] = None
@@ -197,6 +210,10 @@ def lib() -> C.CDLL:
         "rt2_scene_set_variant": (C.c_int, [P, C.c_int]),
         "rt2_scene_set_traversal": (C.c_int, [P, C.c_int]),
         "rt2_scene_set_frame_split": (C.c_int, [P, C.c_int]),
+        "rt2_scene_set_textures": (C.c_int, [P, C.POINTER(Image), I32]),
+        "rt2_image_load": (C.c_int, [C.c_char_p, I32, C.POINTER(Image)]),
+        "rt2_image_free": (None, [C.POINTER(Image)]),
+        "rt2_sd_texture": (C.c_int, [P, I32, C.POINTER(Image)]),
         "rt2_sd_create": (P, []),
         "rt2_sd_destroy": (None, [P]),
         "rt2_sd_load_obj_folder": (C.c_int, [P, C.c_char_p]),
@@ -332,6 +349,15 @@ class SceneData:
     def texture_names(self) -> list:
         return [lib().rt2_sd_texture_name(self._p, i).decode() for i in range(lib().rt2_sd_num_textures(self._p))]
 
+    def texture(self, i: int) -> np.ndarray:
+        """Decoded texture i as (height, width, channels) uint8, row 0 first (flipped on load)."""
+        im = Image()
+        _check(lib().rt2_sd_texture(self._p, i, C.byref(im)), "rt2_sd_texture")
+        return _image_array(im)
+
+    def textures(self) -> list:
+        return [self.texture(i) for i in range(lib().rt2_sd_num_textures(self._p))]
+
     def _view(self, ptr, n, dtype) -> np.ndarray:
         if n == 0:
             return np.zeros(0, dtype=dtype)
@@ -363,6 +389,22 @@ def camera_uniforms(cam: CameraDesc, u: Optional[Uniforms] = None) -> Uniforms:
     u = u or Uniforms()
     _check(lib().rt2_camera_uniforms(C.byref(cam), C.byref(u)), "camera")
     return u
+
+
+def _image_array(im: Image) -> np.ndarray:
+    n = im.width * im.height * im.channels
+    buf = (C.c_uint8 * n).from_address(C.addressof(im.pixels.contents))
+    return np.frombuffer(buf, dtype=np.uint8).copy().reshape(im.height, im.width, im.channels)
+
+
+def load_image(path: str, flip_vertically: bool = True) -> np.ndarray:
+    """rt2_image_load: stbi_load(path, ..., 0) as Texture2D uses it -> (h, w, channels) uint8."""
+    im = Image()
+    _check(lib().rt2_image_load(path.encode(), int(bool(flip_vertically)), C.byref(im)), "rt2_image_load")
+    try:
+        return _image_array(im)
+    finally:
+        lib().rt2_image_free(C.byref(im))
 
 
 def offline_uniforms(width, height, max_bounce, rays_per_pixel, num_triangles, num_textures=0) -> Uniforms:
@@ -424,6 +466,17 @@ class Scene:
     def set_frame_split(self, enable: bool) -> None:
         """(frame, pixel) work items for multi-frame renders (rt2_scene_set_frame_split)."""
         _check(lib().rt2_scene_set_frame_split(self._p, int(bool(enable))), "set_frame_split")
+
+    def set_textures(self, images) -> None:
+        """Uploads textures (list of (h, w, channels) uint8 arrays, stb layout) — the
+        reference's texture units 0..4 (rt2_scene_set_textures)."""
+        arrs = [np.ascontiguousarray(a, dtype=np.uint8) for a in images]
+        arrs = [a if a.ndim == 3 else a[..., None] for a in arrs]
+        ims = (Image * max(len(arrs), 1))()
+        for i, a in enumerate(arrs):
+            ims[i].width, ims[i].height, ims[i].channels = a.shape[1], a.shape[0], a.shape[2]
+            ims[i].pixels = a.ctypes.data_as(C.POINTER(C.c_uint8))
+        _check(lib().rt2_scene_set_textures(self._p, ims, len(arrs)), "rt2_scene_set_textures")
 
     def render(self, u: Uniforms, frame_begin: int, frame_count: int, sh: Shard, accum_ptr: int,
                accum8_ptr: int = 0, stream: int = 0) -> None:

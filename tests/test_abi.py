@@ -40,7 +40,7 @@ def test_struct_layouts(rt2mod):
 
 def test_abi_version_and_errors(rt2mod):
     L = rt2mod.lib()
-    assert L.rt2_abi_version() == 2
+    assert L.rt2_abi_version() == 3
     sd = rt2mod.SceneData()
     try:
         sd.load_obj_folder("/nonexistent/folder")

@@ -123,8 +123,10 @@ def test_light_emission_glass_highlight_edge(rt2mod, tmp_path):
 def test_textures_index_by_directory_order(rt2mod, tmp_path):
     d = tmp_path / "t"
     os.makedirs(d / "textures")
-    for n in ("b.png", "a.png"):
-        open(d / "textures" / n, "wb").close()
+    golden = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "images")
+    for n, src in (("b.png", "rgb8.png"), ("a.png", "gray8.png")):
+        with open(os.path.join(golden, src), "rb") as f, open(d / "textures" / n, "wb") as g:
+            g.write(f.read())
     write(d, "m.mtl", "newmtl T\nmap_Kd a.png\nnewmtl L\nKe 1 1 1\nmap_Kd b.png\n")
     write(d, "m.obj", "mtllib m.mtl\nv 0 0 0\nv 1 0 0\nv 0 1 0\nusemtl T\nf 1 2 3\n")
     sd = load(rt2mod, d)
@@ -135,6 +137,20 @@ def test_textures_index_by_directory_order(rt2mod, tmp_path):
     T, L = m[2], m[1]
     assert T["materialType"] == rt2mod.TEXTURE and T["textureIndex"] == names.index("a.png")
     assert L["materialType"] == rt2mod.LIGHT and L["textureIndex"] == -1  # lights ignore map_Kd
+    # decoded and flipped on load, like Texture2D(path)
+    assert sd.texture(names.index("a.png")).shape == (7, 13, 1)
+    assert np.array_equal(sd.texture(names.index("b.png")),
+                          rt2mod.load_image(os.path.join(golden, "rgb8.png"), flip_vertically=True))
+
+
+def test_undecodable_texture_is_an_error(rt2mod, tmp_path):
+    # Texture2D(path) throws when stbi_load fails (textureClass.cpp:96-101)
+    d = tmp_path / "u"
+    os.makedirs(d / "textures")
+    (d / "textures" / "x.png").write_bytes(b"")
+    write(d, "m.obj", "v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 3\n")
+    with pytest.raises(rt2mod.RT2Error, match="x.png"):
+        load(rt2mod, d)
 
 
 @pytest.mark.parametrize("files,err", [
