@@ -342,6 +342,87 @@ __device__ __forceinline__ void sweep_masked(const f3& o, const f3& d, const flo
     }
 }
 
+// Ballot sweep: phase 1 computes G filters and turns them into wave masks
+// (__ballot); phase 2 runs only when any mask is set, one scalar branch per G
+// triangles in the common case.
+__device__ __forceinline__ void load_tri_smem(const float* gtri, int i, float4& t0, float4& t1, float4& t2) {
+    cfloat* t = (cfloat*)gtri + 12 * i;
+    t0 = ldc4(t);
+    t1 = ldc4(t + 4);
+    t2 = ldc4(t + 8);
+}
+template <int G>
+__device__ __forceinline__ void sweep_ballot(const f3& o, const f3& d, const float* gtri, int count, float& best,
+                                             int& bi, float& bestK) {
+    int i = 0;
+    const unsigned long long me = 1ull << lane_id();
+    for (; i + G <= count; i += G) {
+        MtQ q[G];
+        unsigned long long m[G], any = 0;
+#pragma unroll
+        for (int k = 0; k < G; k++) {
+            float4 t0, t1, t2;
+            load_tri_smem(gtri, i + k, t0, t1, t2);
+            q[k] = mt_quantities(o, d, t0, t1, t2);
+            m[k] = __ballot(mt_pass(q[k], bestK));
+            any |= m[k];
+        }
+        if (__builtin_expect(any != 0, 0)) {
+#pragma unroll
+            for (int k = 0; k < G; k++)
+                if (m[k] & me) mt_exact(q[k], i + k, best, bi, bestK);
+        }
+    }
+    for (; i < count; i++) {
+        float4 t0, t1, t2;
+        load_tri_smem(gtri, i, t0, t1, t2);
+        const MtQ q = mt_quantities(o, d, t0, t1, t2);
+        if (mt_pass(q, bestK)) mt_exact(q, i, best, bi, bestK);
+    }
+}
+
+// VALU-only form of mt_pass: the five conditions as signed slacks whose
+// minimum is >= 0 exactly when all hold (RN(x - y) has the sign of x - y;
+// tnum > 0 as tnum - 2^-149 >= 0).  Conservative under flush-to-zero and NaN
+// as well (both can only make it pass more).
+__device__ __forceinline__ bool mt_pass_min(const MtQ& q, float bestK) {
+    const float B = q.det * 0x1p-60f;
+    const float D = q.det * 1.0009765625f;
+    const float K = q.det * bestK;
+    const float m1 = fminf(fminf(B - q.U, q.V + B), D - (q.V - q.U));
+    const float m2 = fminf(K - q.tnum, q.tnum - 0x1p-149f);
+    return fminf(m1, m2) >= 0.0f;
+}
+template <int G>
+__device__ __forceinline__ void sweep_minfilter(const f3& o, const f3& d, const float* gtri, int count, float& best,
+                                                int& bi, float& bestK) {
+    int i = 0;
+    const unsigned long long me = 1ull << lane_id();
+    for (; i + G <= count; i += G) {
+        MtQ q[G];
+        unsigned long long m[G], any = 0;
+#pragma unroll
+        for (int k = 0; k < G; k++) {
+            float4 t0, t1, t2;
+            load_tri_smem(gtri, i + k, t0, t1, t2);
+            q[k] = mt_quantities(o, d, t0, t1, t2);
+            m[k] = __ballot(mt_pass_min(q[k], bestK));
+            any |= m[k];
+        }
+        if (__builtin_expect(any != 0, 0)) {
+#pragma unroll
+            for (int k = 0; k < G; k++)
+                if (m[k] & me) mt_exact(q[k], i + k, best, bi, bestK);
+        }
+    }
+    for (; i < count; i++) {
+        float4 t0, t1, t2;
+        load_tri_smem(gtri, i, t0, t1, t2);
+        const MtQ q = mt_quantities(o, d, t0, t1, t2);
+        if (mt_pass(q, bestK)) mt_exact(q, i, best, bi, bestK);
+    }
+}
+
 // Lean masked sweep: like sweep_masked, but phase 1 keeps ONLY the G filter
 // lane-masks (SGPRs) live; phase 2 (entered for ~5% of groups on config B)
 // reloads the surviving triangle and recomputes its intermediates.  Frees the
@@ -829,7 +910,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             float best = 1e38f, bestK = 1e38f * 1.0009765625f;
             int bi = -1;
             const f3 o = L.o, d = L.d;
-            if constexpr (G >= 200)
+            if constexpr (G >= 400)
+                sweep_minfilter<G - 400>(o, d, (const float*)p.tri, p.n_tris, best, bi, bestK);
+            else if constexpr (G >= 300)
+                sweep_ballot<G - 300>(o, d, (const float*)p.tri, p.n_tris, best, bi, bestK);
+            else if constexpr (G >= 200)
                 sweep_lean<G - 200, true>(o, d, nullptr, (const float*)p.tri, p.n_tris, 0, best, bi, bestK);
             else if constexpr (G >= 100)
                 sweep_masked<G - 100, true>(o, d, nullptr, p.tri ? (const float*)p.tri : nullptr, p.n_tris, 0, best,
@@ -1227,15 +1312,54 @@ __device__ __forceinline__ float slab64(const TravState3& T, float b0x, float b0
     return (tMin >= tMax || tMax < 0.0f) ? 1e38f : tMin;
 }
 
+// DIV == 2: decision filter for the slab tests.  t' = RN(n*y) is within
+// 2^-21 * max(|t|, |t'|) of the exact t = RN(n/d) (y = RN(1/d): |n*y - n/d| <=
+// 2^-24 |n/d|, plus two half-ulp roundings), has the same sign, and is 0 iff
+// t is; min/max keep that bound.  Every decision the traversal takes from the
+// box distances (a box missed: tMin >= tMax or tMax < 0; near/far: dA < dB;
+// push: d < best) is taken from the t' values when the two compared numbers
+// are further apart than 2^-19 * (|a| + |b|) — then the exact values order
+// the same way — and the lane re-runs the exact slab_fast otherwise.
+__device__ __forceinline__ void slab_approx(const SlabRay& R, float b0x, float b0y, float b0z, float b1x, float b1y,
+                                            float b1z, float& tMin, float& tMax) {
+    const float x0 = (b0x - R.o.x) * R.y.x, x1 = (b1x - R.o.x) * R.y.x;
+    const float y0 = (b0y - R.o.y) * R.y.y, y1 = (b1y - R.o.y) * R.y.y;
+    const float z0 = (b0z - R.o.z) * R.y.z, z1 = (b1z - R.o.z) * R.y.z;
+    tMin = fmaxf(fmaxf(fmaxf(-1e32f, fminf(x0, x1)), fminf(y0, y1)), fminf(z0, z1));
+    tMax = fminf(fminf(fminf(1e32f, fmaxf(x0, x1)), fmaxf(y0, y1)), fmaxf(z0, z1));
+}
+__device__ __forceinline__ bool near_tie(float a, float b) { return fabsf(a - b) <= (fabsf(a) + fabsf(b)) * 0x1p-19f; }
+
 template <int BLOCK, int DIV>
 __device__ __forceinline__ void bvh_interior3(TravState3& T, int* st, int e, const float4* __restrict__ recs,
-                                              bool fast, int stack_slots, uint32_t& visits) {
+                                              bool fast, int stack_slots, uint32_t& visits, uint32_t& refined) {
     visits++;
     const float4* rp = recs + 4 * e;
     const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
     const float4 r3 = rp[3];
     float dA, dB;
-    if (fast && DIV == 1) {
+    bool exact = true;
+    if (fast && DIV == 2) {
+        float aMin, aMax, bMin, bMax;
+        slab_approx(T.R, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, aMin, aMax);
+        slab_approx(T.R, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, bMin, bMax);
+        const bool hitA = !(aMin >= aMax || aMax < 0.0f), hitB = !(bMin >= bMax || bMax < 0.0f);
+        dA = hitA ? aMin : 1e38f;
+        dB = hitB ? bMin : 1e38f;
+        // a box flat on some axis (bmin == bmax there) is missed in both
+        // arithmetics: that axis puts the same t into tMin's max and tMax's min
+        const bool flatA = (r0.x == r0.w) | (r0.y == r1.x) | (r0.z == r1.y);
+        const bool flatB = (r1.z == r2.y) | (r1.w == r2.z) | (r2.x == r2.w);
+        bool amb = (near_tie(aMin, aMax) & !flatA) | (near_tie(bMin, bMax) & !flatB);
+        amb |= hitA & hitB & near_tie(dA, dB);
+        amb |= hitA & near_tie(dA, T.best);
+        amb |= hitB & near_tie(dB, T.best);
+        exact = amb;
+        refined += amb ? 1u : 0u;
+    }
+    if (!exact) {
+        // decisions taken from the filtered distances
+    } else if (fast && DIV == 1) {
         dA = slab64(T, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y);
         dB = slab64(T, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w);
     } else if (fast) {
@@ -1272,7 +1396,7 @@ __device__ __forceinline__ void bvh_leaf3(TravState3& T, int e, const rt2_node* 
     }
 }
 
-template <int BLOCK, int THRESH, int DIV, int WPE>
+template <int BLOCK, int THRESH, int DIV, int WPE, int DIAG = 0>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void render_bvh3(RenderParams p) {
     extern __shared__ int bvh_stack[];
     int* st = bvh_stack + threadIdx.x;
@@ -1285,8 +1409,17 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     T.bi = -1;
     T.fast = true;
     T.yx = T.yy = T.yz = 0.0;
-    uint32_t tests = 0, visits = 0;
+    uint32_t tests = 0, visits = 0, refined = 0;
+    // DIAG: wave-uniform tallies (lane 0 publishes them): [0] inner iterations,
+    // [1] lanes in the interior sub-step, [2] lanes in the leaf sub-step,
+    // [3] finished lanes waiting, [4] DONE lanes, [5] outer iterations,
+    // [6] lanes shading, [7] iterations running the interior body
+    unsigned long long dg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (;;) {
+        if constexpr (DIAG) {
+            dg[5] += 1;
+            dg[6] += __popcll(__ballot(T.sp < 0));
+        }
         if (T.sp < 0) {
             shade(L, p, T.best, T.bi);
             T.sp = 0;
@@ -1296,16 +1429,26 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
         if (!__any(T.sp > 0)) break;
         const bool fast = (DIV == 1 || p.recs_ok) && __all(T.fast || T.sp <= 0);
         for (;;) {
+            if constexpr (DIAG) {
+                dg[0] += 1;
+                const bool in = T.sp > 0 && st[(T.sp - 1) * BLOCK] >= 0;
+                const unsigned long long bi = __ballot(in);
+                dg[1] += __popcll(bi);
+                dg[7] += bi ? 1 : 0;
+                dg[3] += __popcll(__ballot(T.sp < 0));
+                dg[4] += __popcll(__ballot(L.st == ST_DONE));
+            }
             // interior sub-step
             if (T.sp > 0) {
                 const int e = st[(T.sp - 1) * BLOCK];
                 if (e >= 0) {
                     T.sp -= 1;
-                    bvh_interior3<BLOCK, DIV>(T, st, e, recs, fast, p.stack_slots, visits);
+                    bvh_interior3<BLOCK, DIV>(T, st, e, recs, fast, p.stack_slots, visits, refined);
                     if (T.sp == 0) T.sp = -1;
                 }
             }
             // leaf sub-step
+            if constexpr (DIAG) dg[2] += __popcll(__ballot(T.sp > 0 && st[(T.sp - 1) * BLOCK] < 0));
             if (T.sp > 0) {
                 const int e = st[(T.sp - 1) * BLOCK];
                 if (e < 0) {
@@ -1319,14 +1462,18 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
         }
     }
     flush_counters(L, p);
-    unsigned long long t = tests, v = visits;
+    unsigned long long t = tests, v = visits, rf = refined;
     for (int off = 32; off > 0; off >>= 1) {
         t += __shfl_xor(t, off);
         v += __shfl_xor(v, off);
+        rf += __shfl_xor(rf, off);
     }
     if (lane_id() == 0) {
-        atomicAdd(p.seg_counter + 1, t);  // leaf triangle tests
-        atomicAdd(p.seg_counter + 2, v);  // interior node visits (diagnostic)
+        atomicAdd(p.seg_counter + 1, t);   // leaf triangle tests
+        atomicAdd(p.seg_counter + 2, v);   // interior node visits (diagnostic)
+        atomicAdd(p.seg_counter + 3, rf);  // DIV 2: visits re-run exactly (diagnostic)
+        if constexpr (DIAG)
+            for (int k = 0; k < 8; k++) atomicAdd(p.seg_counter + 7 + k, dg[k]);  // counters [8..15]
         // wave finish-time spread (diagnostic): [6] earliest, [7] latest wave end, 10 ns ticks
         const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
         atomicMin(p.seg_counter + 5, t_end);
@@ -1357,7 +1504,12 @@ __global__ void div_check_kernel(uint32_t seed, unsigned long long count, int mo
         float d = __uint_as_float(((g << 8) & 0x80000000u) | (de << 23) | ((h * 2246822519u) & 0x7fffffu));
         if (fabsf(d) < 1e-6f) d = copysignf(1e-6f, d);
         if (fabsf(d) > 2.0f) d = copysignf(2.0f, d);
-        const float q = mode == 1 ? div64(n, 1.0 / (double)d) : div_mk(n, d, 1.0f / d);
+        float q;
+        if (mode == 1) {
+            q = div64(n, 1.0 / (double)d);
+        } else {
+            q = div_mk(n, d, 1.0f / d);
+        }
         const float ref = n / d;
         if (__float_as_uint(q) != __float_as_uint(ref)) {
             nbad++;
@@ -1605,6 +1757,7 @@ void set_error(const std::string& msg);
         }                                                                                      \
     } while (0)
 
+constexpr int kCounters = 32;  // [0] items, [1..7] stats + wave-end, [8..] kernel diagnostics
 struct rt2_scene {
     int device = 0;
     int n_tris = 0, n_mats = 0, n_nodes = 0;
@@ -1629,7 +1782,7 @@ struct rt2_scene {
     int traversal = RT2_TRAVERSAL_BRUTE;
     int bvh_depth = 0;              // longest root-to-leaf path (nodes)
     int last_kind = 0;              // kind of the last launch (stats: tests)
-    unsigned long long diag[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long diag[kCounters] = {};
     int num_cus = 256;
     size_t max_lds = 65536;
 };
@@ -1834,8 +1987,8 @@ extern "C" int rt2_scene_create(const rt2_triangle* tris, int32_t n_tris, const 
     HIPCHECK(hipMalloc(&s->d_tri, nt * 3 * sizeof(float4)));
     HIPCHECK(hipMalloc(&s->d_mtl, nt * sizeof(int)));
     HIPCHECK(hipMalloc(&s->d_mats, (size_t)n_mats * sizeof(rt2_material)));
-    HIPCHECK(hipMalloc(&s->d_counters, 8 * sizeof(unsigned long long)));
-    HIPCHECK(hipMemset(s->d_counters, 0, 8 * sizeof(unsigned long long)));
+    HIPCHECK(hipMalloc(&s->d_counters, kCounters * sizeof(unsigned long long)));
+    HIPCHECK(hipMemset(s->d_counters, 0, kCounters * sizeof(unsigned long long)));
     if (n_tris > 0) HIPCHECK(hipMemcpy(s->d_raw, tris, (size_t)n_tris * sizeof(rt2_triangle), hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(s->d_mats, mats, (size_t)n_mats * sizeof(rt2_material), hipMemcpyHostToDevice));
     if (s->n_nodes > 0) {
@@ -1934,8 +2087,8 @@ hipError_t launch_t(const RenderParams& p, int blocks, size_t lds, hipStream_t s
     else if constexpr (KIND == K_BVH2)
         hipLaunchKernelGGL((render_bvh2<BLOCK, MT>), dim3(blocks), dim3(BLOCK), lds, st, p);
     else if constexpr (KIND == K_BVH3)
-        hipLaunchKernelGGL((render_bvh3<BLOCK, MT % 1000, MT / 1000, UNROLL>), dim3(blocks), dim3(BLOCK), lds, st,
-                           p);
+        hipLaunchKernelGGL((render_bvh3<BLOCK, MT % 1000, (MT / 1000) % 10, UNROLL, MT / 10000>), dim3(blocks),
+                           dim3(BLOCK), lds, st, p);
     else
         hipLaunchKernelGGL((render_resident<BLOCK, MT, UNROLL>), dim3(blocks), dim3(BLOCK), lds, st, p);
     return hipGetLastError();
@@ -1952,8 +2105,8 @@ hipError_t occ_t(int* occ, size_t lds) {
     else if constexpr (KIND == K_BVH2)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_bvh2<BLOCK, MT>, BLOCK, lds);
     else if constexpr (KIND == K_BVH3)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_bvh3<BLOCK, MT % 1000, MT / 1000, UNROLL>, BLOCK,
-                                                            lds);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            occ, render_bvh3<BLOCK, MT % 1000, (MT / 1000) % 10, UNROLL, MT / 10000>, BLOCK, lds);
     else
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_resident<BLOCK, MT, UNROLL>, BLOCK, lds);
 }
@@ -2015,6 +2168,15 @@ const Variant kVariants[] = {
     RT2_VARIANT(K_SMEM, 256, 32108, 6, "smem/256/masked8/coop32/w6"), // 52
     RT2_VARIANT(K_BVH3, 256, 16, 5, "bvh3/256/t16/w5"),              // 53
     RT2_VARIANT(K_BVH3, 256, 8, 5, "bvh3/256/t8/w5"),                // 54
+    RT2_VARIANT(K_BVH3, 256, 2016, 5, "bvh3/256/t16/filt/w5"),       // 55
+    RT2_VARIANT(K_BVH3, 256, 2008, 5, "bvh3/256/t8/filt/w5"),        // 56
+    RT2_VARIANT(K_BVH3, 256, 2016, 1, "bvh3/256/t16/filt"),          // 57
+    RT2_VARIANT(K_BVH3, 256, 10016, 5, "bvh3/256/t16/w5/DIAG"),      // 58: diagnostic counters
+    RT2_VARIANT(K_SMEM, 256, 32308, 1, "smem/256/ballot8/coop32"),   // 59
+    RT2_VARIANT(K_SMEM, 256, 32408, 1, "smem/256/minfilt8/coop32"),  // 60
+    RT2_VARIANT(K_SMEM, 256, 32304, 1, "smem/256/ballot4/coop32"),   // 61
+    RT2_VARIANT(K_SMEM, 256, 32416, 1, "smem/256/minfilt16/coop32"), // 62
+    RT2_VARIANT(K_SMEM, 256, 32404, 1, "smem/256/minfilt4/coop32"),  // 63
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr size_t kResidentMaxBytes = 112 * 1024;
@@ -2182,7 +2344,7 @@ extern "C" int rt2_scene_stats(rt2_scene* s, rt2_stats* out, int reset) {
     }
     HIPCHECK(hipSetDevice(s->device));
     HIPCHECK(hipDeviceSynchronize());
-    unsigned long long c[8];
+    unsigned long long c[kCounters];
     HIPCHECK(hipMemcpy(c, s->d_counters, sizeof(c), hipMemcpyDeviceToHost));
     std::memcpy(s->diag, c, sizeof(c));
     out->samples = s->samples;
@@ -2283,9 +2445,16 @@ extern "C" int rt2_render_host(rt2_scene* s, const rt2_uniforms* u, uint32_t fra
 // Not in rt2.h (diagnostics): counters of the last rt2_scene_stats call
 // [1] segments, [2] groups, [3] groups with survivors, [4] exact iterations,
 // [5] lane survivors (STATS variants only), and the variant last launched.
+// Not in rt2.h (diagnostics): all kCounters counters of the last stats call.
+extern "C" int rt2_scene_diag_ex(rt2_scene* s, unsigned long long* out, int n) {
+    if (!s || !out || n < 0) return -1;
+    std::memcpy(out, s->diag, sizeof(unsigned long long) * (size_t)std::min(n, kCounters));
+    return std::min(n, kCounters);
+}
+
 extern "C" int rt2_scene_diag(rt2_scene* s, unsigned long long* out8, int* last_variant) {
     if (!s || !out8) return -1;
-    std::memcpy(out8, s->diag, sizeof(s->diag));
+    std::memcpy(out8, s->diag, 8 * sizeof(unsigned long long));
     if (last_variant) *last_variant = s->last_variant;
     return 0;
 }

@@ -52,6 +52,7 @@ for rnd in range(a.rounds):
         if a.traversal == "bvh":
             diag[v] = dict(segments=c[1], tests_per_segment=c[2] / max(c[1], 1),
                            interior_visits_per_segment=c[3] / max(c[1], 1),
+                           refined_visit_frac=c[4] / max(c[3], 1),
                            wave_end_spread_ms=(c[7] - c[6]) * 1e-5 if c[7] > c[6] else None)
         elif c[2]:
             diag[v] = dict(segments=c[1], groups=c[2], groups_with_survivor=c[3], exact_iters=c[4],

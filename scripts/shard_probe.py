@@ -1,0 +1,52 @@
+"""Predicts strong-scaling efficiency on one GPU: renders the slab that rank 0
+of N would own (rt2_shard {tile_rows, 0, N}) and compares its kernel time with
+1/N of the whole image.  (The 8-GPU run itself is the driver's; this shows
+whether a 1/N slab still fills the chip.)"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "raytracing2-fork_amd"))
+import torch  # noqa: E402,F401
+import rt2  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="B")
+ap.add_argument("--traversal", default="brute")
+ap.add_argument("--tile-rows", type=int, default=1)
+ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--variants", default="0")
+a = ap.parse_args()
+sd, spec = rt2.build_config_scene(a.config)
+u = rt2.offline_uniforms(spec.width, spec.height, spec.bounces, spec.rays, sd.num_triangles)
+scene = rt2.Scene(sd, 0)
+scene.set_traversal(a.traversal)
+
+
+def slab_time(sh):
+    rows = rt2.shard_rows(spec.height, sh)
+    acc = torch.zeros((rows, spec.width, 4), device="cuda")
+    scene.render(u, 0, spec.frames, sh, acc.data_ptr())
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(a.reps):
+        acc.zero_()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        scene.render(u, 0, spec.frames, sh, acc.data_ptr())
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t)
+    return min(ts)
+
+
+for var in [int(v) for v in a.variants.split(",")]:
+    scene.set_variant(var)
+    out = {n: slab_time(rt2.shard(a.tile_rows, 0, n)) for n in (1, 2, 4, 8)}
+    base = out[1]
+    print(json.dumps({"config": a.config, "traversal": a.traversal, "tile_rows": a.tile_rows, "variant": var,
+                      "name": rt2.lib().rt2_variant_name(var).decode() if var else "auto",
+                      "slab_ms": {n: round(t * 1e3, 2) for n, t in out.items()},
+                      "predicted_efficiency": {n: round(base / n / t, 3) for n, t in out.items()}}), flush=True)
