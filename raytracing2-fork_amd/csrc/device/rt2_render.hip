@@ -503,6 +503,55 @@ __device__ __forceinline__ void coop_closest(const f3& o, const f3& d, const flo
     bi_out = bi;
 }
 
+// Team sweep (tail mode): the n live rays of a wave each get a team of
+// k = 64 / 2^ceil(log2 n) lanes; member j of a team tests triangles j, j+k,
+// j+2k, ... of its ray (vector loads: the k members read k consecutive
+// records, every team the same ones), then the team reduces (dst, index)
+// lexicographically — the sequential strict `dst < best` scan's result.  A
+// segment of every live ray costs N/k tests per lane instead of N, so the
+// last rays of a launch (and small per-GPU slabs) finish up to k times sooner.
+// Returns the closest hit of the calling lane's own ray (live lanes).
+__device__ __forceinline__ void team_closest(const f3& lo, const f3& ld, const float4* tris, int n_tris,
+                                             unsigned long long act, float& best_out, int& bi_out) {
+    const int n = __popcll(act);
+    const int lg = n <= 1 ? 0 : 32 - __builtin_clz((unsigned)(n - 1));
+    const int k = 64 >> lg;
+    const int me = (int)lane_id();
+    const int t = me / k, j = me - t * k;
+    // the t-th live lane of the wave: the lane whose live-rank is t
+    int leader = 0;
+    {
+        unsigned long long m = act;
+        for (int r = 0; r < t && m; r++) m &= m - 1;
+        leader = m ? __builtin_ctzll(m) : 0;
+    }
+    const bool member = t < n;
+    const f3 o = mk(__shfl(lo.x, leader), __shfl(lo.y, leader), __shfl(lo.z, leader));
+    const f3 d = mk(__shfl(ld.x, leader), __shfl(ld.y, leader), __shfl(ld.z, leader));
+    float best = 1e38f, bestK = 1e38f * 1.0009765625f;
+    int bi = -1;
+    if (member) {
+        for (int i = j; i < n_tris; i += k) {
+            const float4* tp = tris + 3 * i;
+            const MtQ q = mt_quantities(o, d, tp[0], tp[1], tp[2]);
+            if (mt_pass(q, bestK)) mt_exact(q, i, best, bi, bestK);
+        }
+    }
+    for (int off = 1; off < k; off <<= 1) {
+        const float ob = __shfl_xor(best, off);
+        const int oi = __shfl_xor(bi, off);
+        const bool take = (ob < best) || (ob == best && oi >= 0 && (bi < 0 || oi < bi));
+        if (take) {
+            best = ob;
+            bi = oi;
+        }
+    }
+    // each live lane reads its team's result (team index = its live rank)
+    const int src = (int)lanes_below(act) * k;
+    best_out = __shfl(best, src);
+    bi_out = __shfl(bi, src);
+}
+
 template <int MT>
 __device__ __forceinline__ void mt_dispatch(const f3& o, const f3& d, float4 t0, float4 t1, float4 t2, int idx,
                                             float& best, int& best_i, float& bestK) {
@@ -880,7 +929,18 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
         advance(L, p);
         const unsigned long long act = __ballot(L.st == ST_TRACE);
         if (!act) break;
-        if (COOP > 0 && __popcll(act) <= (unsigned)COOP && __any(L.st == ST_DONE)) {
+        if (COOP >= 100 && __popcll(act) <= (unsigned)(COOP - 100) && __any(L.st == ST_DONE)) {
+            float b;
+            int bidx;
+            team_closest(L.o, L.d, p.tri, p.n_tris, act, b, bidx);
+            if (L.st == ST_TRACE) {
+                L.bounce += 1;
+                L.segs += 1;
+                shade(L, p, b, bidx);
+            }
+            continue;
+        }
+        if (COOP > 0 && COOP < 100 && __popcll(act) <= (unsigned)COOP && __any(L.st == ST_DONE)) {
             float mybest = 1e38f;
             int mybi = -1;
             unsigned long long m = act;
@@ -2177,6 +2237,9 @@ const Variant kVariants[] = {
     RT2_VARIANT(K_SMEM, 256, 32304, 1, "smem/256/ballot4/coop32"),   // 61
     RT2_VARIANT(K_SMEM, 256, 32416, 1, "smem/256/minfilt16/coop32"), // 62
     RT2_VARIANT(K_SMEM, 256, 32404, 1, "smem/256/minfilt4/coop32"),  // 63
+    RT2_VARIANT(K_SMEM, 256, 132108, 1, "smem/256/masked8/team32"),  // 64
+    RT2_VARIANT(K_SMEM, 256, 148108, 1, "smem/256/masked8/team48"),  // 65
+    RT2_VARIANT(K_SMEM, 256, 164108, 1, "smem/256/masked8/team64"),  // 66
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr size_t kResidentMaxBytes = 112 * 1024;

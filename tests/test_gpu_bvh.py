@@ -180,3 +180,19 @@ def test_bvh2_big_leaves_and_single_node(rt2mod, oraclemod, torch_cuda):
                 scene.set_variant(v)
                 img = scene.render_host(u, 0, 1)
                 assert_exact(img, acc[..., :3], f"variant {v} n={n_tris} nodes={len(nd)}")
+
+
+@pytest.mark.parametrize("traversal", ["brute", "bvh"])
+def test_config_E_million_triangles(rt2mod, oraclemod, config_scene, torch_cuda, traversal):
+    """Config E (1,000,014 triangles, mirror box, 16 bounces) at a small image:
+    both traversals bit-exact against the oracle (brute: the tiled kernel)."""
+    sd, spec = config_scene("E")
+    W, H = (12, 8) if traversal == "brute" else (48, 32)
+    u = rt2mod.offline_uniforms(W, H, spec.bounces, 2, sd.num_triangles)
+    scene = rt2mod.Scene(sd, 0)
+    scene.set_traversal(traversal)
+    img = scene.render_host(u, 0, 1)
+    st = scene.stats(reset=True)
+    ref, _, segs = oracle_mean(oraclemod, sd, u, np.arange(H), 0, 1, traversal)
+    assert_exact(img, ref, f"config E {traversal}")
+    assert st.segments == segs

@@ -254,3 +254,38 @@ def test_frame_split_identical(rt2mod, oraclemod, config_scene, torch_cuda, trav
     assert np.array_equal(out[False][1], out[True][1])
     ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(H), 2, F, traversal)
     assert_exact(out[True][0], ref, f"split {traversal}")
+
+
+# brute-force kernel variants that change the schedule, not the arithmetic:
+# masked/ballot/min-filter sweeps, cooperative and team tail modes, occupancy hints
+BRUTE_VARIANTS = [0, 1, 2, 22, 24, 28, 31, 52, 59, 60, 64, 65, 66]
+
+
+@pytest.mark.parametrize("variant", BRUTE_VARIANTS)
+def test_brute_variants_bit_exact(rt2mod, oraclemod, config_scene, torch_cuda, variant):
+    sd, spec = config_scene("B")
+    W, H, R = 96, 54, 4
+    u = rt2mod.offline_uniforms(W, H, spec.bounces, R, sd.num_triangles)
+    scene = rt2mod.Scene(sd, 0)
+    scene.set_variant(variant)
+    img = scene.render_host(u, 0, 2)
+    st = scene.stats(reset=True)
+    ref, _, segs = oracle_mean(oraclemod, sd, u, np.arange(H), 0, 2)
+    assert_exact(img, ref, f"variant {variant}")
+    assert st.segments == segs
+
+
+@pytest.mark.parametrize("variant", [64, 66])
+def test_team_tail_small_slab(rt2mod, oraclemod, config_scene, torch_cuda, variant):
+    """A slab smaller than the number of lanes (rank 5 of 8, tiles of 3 rows):
+    the team mode runs from the first segment."""
+    sd, spec = config_scene("B")
+    W, H = 160, 90
+    u = rt2mod.offline_uniforms(W, H, spec.bounces, 8, sd.num_triangles)
+    sh = rt2mod.shard(3, 5, 8)
+    scene = rt2mod.Scene(sd, 0)
+    scene.set_variant(variant)
+    img = scene.render_host(u, 0, 1, sh)
+    rows = rt2mod.shard_row_ids(H, sh)
+    ref, _, _ = oracle_mean(oraclemod, sd, u, rows, 0, 1)
+    assert_exact(img, ref, f"team variant {variant} slab")
