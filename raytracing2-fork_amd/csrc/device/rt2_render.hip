@@ -52,6 +52,9 @@ struct RenderParams {
     unsigned long long n_items;  // work items: pixels, or frames x pixels when frame_split
     unsigned long long n_pix;    // pixels of the shard
     int frame_split;             // 1: item = (frame, pixel), frame-major; colours -> frame_buf
+    const uint32_t* order;       // nullable: run rank -> run of 64 pixels (most expensive first)
+    uint32_t n_runs;             // full 64-pixel runs covered by `order` (the partial last run keeps its place)
+    uint32_t* cost_out;          // nullable: per-pixel item cost (shader clocks) for the next launch's order
     float4* frame_buf;           // frame_split: [frame_count][n_pix] per-frame colours
     float4* accum;
     uint4* accum8;
@@ -575,6 +578,7 @@ struct Lane {
     bool inside;
     f3 o, d, rayColor, incoming, colorCum;
     uint32_t segs;
+    uint32_t t0;  // item start (s_memtime low bits), for the cost map
 };
 
 __device__ __forceinline__ void end_path(Lane& L, const RenderParams& p);
@@ -597,6 +601,8 @@ __device__ __forceinline__ void advance(Lane& L, const RenderParams& p) {
                     const uint32_t it32 = (uint32_t)it, np32 = (uint32_t)p.n_pix;
                     const uint32_t f = p.frame_split ? it32 / np32 : 0u;
                     L.item = it32 - f * np32;
+                    if (p.order && L.item < p.n_runs * 64u) L.item = p.order[L.item >> 6] * 64u + (L.item & 63u);
+                    L.t0 = (uint32_t)__builtin_amdgcn_s_memtime();
                     int lr = (int)(L.item / (uint32_t)p.W);
                     L.x = (int)(L.item - (uint32_t)lr * (uint32_t)p.W);
                     L.y = shard_row(lr, p.tile_rows, p.rank, p.nranks);
@@ -652,6 +658,7 @@ __device__ __forceinline__ void end_path(Lane& L, const RenderParams& p) {
     c = mk(srgb1(aces1(c.x)), srgb1(aces1(c.y)), srgb1(aces1(c.z)));
     if (p.frame_split) {  // frame_accumulate adds the frames in order afterwards
         p.frame_buf[(size_t)L.frame * p.n_pix + L.item] = make_float4(c.x, c.y, c.z, 0.0f);
+        if (p.cost_out) p.cost_out[L.item] = (uint32_t)__builtin_amdgcn_s_memtime() - L.t0;
         L.st = ST_NEED_ITEM;
         return;
     }
@@ -667,6 +674,7 @@ __device__ __forceinline__ void end_path(Lane& L, const RenderParams& p) {
     }
     L.frame += 1;
     L.st = L.frame < p.frame_count ? ST_NEW_FRAME : ST_NEED_ITEM;
+    if (L.st == ST_NEED_ITEM && p.cost_out) p.cost_out[L.item] = (uint32_t)__builtin_amdgcn_s_memtime() - L.t0;
 }
 
 // texture(sampler2D, uv) with GL_LINEAR (no mipmaps) + GL_REPEAT, GL 4.3
@@ -809,6 +817,7 @@ __device__ __forceinline__ void lane_init(Lane& L) {
     L.inside = false;
     L.o = L.d = L.rayColor = L.incoming = L.colorCum = mk(0.0f, 0.0f, 0.0f);
     L.segs = 0;
+    L.t0 = 0;
 }
 
 __device__ __forceinline__ void flush_counters(const Lane& L, const RenderParams& p) {
@@ -1737,6 +1746,48 @@ __global__ void frame_accumulate(const float4* __restrict__ fb, unsigned long lo
     if (acc8) acc8[i] = q;
 }
 
+// Cost-ordered scheduling: a counting sort of the pixels by the bit length of
+// their previous item cost (32 buckets, most expensive first).  The order
+// inside a bucket is whatever the atomics produce — it changes only which lane
+// takes which pixel when, never a pixel's arithmetic.
+// Runs of 64 consecutive pixels (one wave's worth of neighbouring pixels,
+// so the lanes of a wave keep coherent rays) are the unit that is ordered.
+__device__ __forceinline__ uint32_t run_cost(const uint32_t* __restrict__ cost, unsigned long long r) {
+    uint32_t c = 0;
+    for (int k = 0; k < 64; k++) c += cost[r * 64 + k] >> 8;
+    return c;
+}
+__global__ void cost_histogram(const uint32_t* __restrict__ cost, unsigned long long n, uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[32];
+    if (threadIdx.x < 32) h[threadIdx.x] = 0;
+    __syncthreads();
+    for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (unsigned long long)gridDim.x * blockDim.x) {
+        const uint32_t c = run_cost(cost, i);
+        atomicAdd(&h[c ? 31 - __clz(c) : 0], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < 32 && h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+}
+__global__ void cost_offsets(uint32_t* hist) {  // one thread: descending exclusive scan, in place
+    if (threadIdx.x != 0) return;
+    uint32_t run = 0;
+    for (int b = 31; b >= 0; b--) {
+        const uint32_t c = hist[b];
+        hist[b] = run;
+        run += c;
+    }
+}
+__global__ void cost_scatter(const uint32_t* __restrict__ cost, unsigned long long n, uint32_t* __restrict__ cursor,
+                             uint32_t* __restrict__ order) {
+    for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (unsigned long long)gridDim.x * blockDim.x) {
+        const uint32_t c = run_cost(cost, i);
+        const uint32_t pos = atomicAdd(&cursor[c ? 31 - __clz(c) : 0], 1u);
+        order[pos] = (uint32_t)i;
+    }
+}
+
 // Pre-transform: RTXTriangle (80 B) -> {a, e0, e1, n} (48 B) + material index.
 __global__ void prep_triangles(const rt2_triangle* tris, int n, float4* out, int* mtl) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1835,6 +1886,15 @@ struct rt2_scene {
     int bvh_root = 0;                           // BVH v2 stack entry of node 0
     int recs_ok = 0;                            // BVH v3 fast-path precondition on the boxes
     int split_frames = 1;                       // frame-major (frame, pixel) items when F > 1
+    int cost_order = 0;                         // order items by the previous launch's per-pixel cost (opt-in)
+    uint32_t* d_cost = nullptr;                 // per-pixel cost map of the last launch
+    uint32_t* d_order = nullptr;                // pixel order for the next launch
+    uint32_t* d_hist = nullptr;                 // 32 counters
+    unsigned long long cost_npix = 0;           // pixels the cost map describes (0 = none)
+    unsigned long long cost_cap = 0;
+    int cost_key[4] = {0, 0, 0, 0};             // W, tile_rows, rank, nranks the map belongs to
+    hipEvent_t last_launch = nullptr;           // renders of one scene are ordered (shared scratch)
+    bool last_launch_valid = false;
     unsigned long long* d_counters = nullptr;  // [0] item counter, [1] segments
     unsigned long long samples = 0, tests_per_seg = 0;
     int variant = 0;
@@ -1991,6 +2051,16 @@ extern "C" int rt2_scene_set_textures(rt2_scene* s, const rt2_image* images, int
     return 0;
 }
 
+extern "C" int rt2_scene_set_cost_order(rt2_scene* s, int enable) {
+    if (!s) {
+        rt2h::set_error("rt2_scene_set_cost_order: null scene");
+        return -1;
+    }
+    s->cost_order = enable ? 1 : 0;
+    s->cost_npix = 0;  // forget the map
+    return 0;
+}
+
 extern "C" int rt2_scene_set_frame_split(rt2_scene* s, int enable) {
     if (!s) {
         rt2h::set_error("rt2_scene_set_frame_split: null scene");
@@ -2098,6 +2168,10 @@ extern "C" void rt2_scene_destroy(rt2_scene* s) {
     (void)hipFree(s->d_nodes);
     (void)hipFree(s->d_recs);
     (void)hipFree(s->d_fb);
+    (void)hipFree(s->d_cost);
+    (void)hipFree(s->d_order);
+    (void)hipFree(s->d_hist);
+    if (s->last_launch) (void)hipEventDestroy(s->last_launch);
     (void)hipFree(s->d_texels);
     (void)hipFree(s->d_tex_desc);
     (void)hipFree(s->d_counters);
@@ -2315,6 +2389,10 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     p.seg_counter = s->d_counters + 1;
     p.tile_tris = kTileTris;
 
+    // renders of one scene share its counters and scratch (frame planes, cost
+    // map, pixel order): a render waits for the scene's previous one, whatever
+    // stream that was issued on
+    if (s->last_launch_valid) HIPCHECK(hipStreamWaitEvent(st, s->last_launch, 0));
     HIPCHECK(hipMemsetAsync(s->d_counters, 0, sizeof(unsigned long long), st));
     HIPCHECK(hipMemsetAsync(s->d_counters + 6, 0xff, sizeof(unsigned long long), st));  // diag: min wave end
     HIPCHECK(hipMemsetAsync(s->d_counters + 7, 0, sizeof(unsigned long long), st));     // diag: max wave end
@@ -2336,6 +2414,9 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
             s->last_kind = K_SMEM;
         }
         HIPCHECK(hipGetLastError());
+        if (!s->last_launch) HIPCHECK(hipEventCreateWithFlags(&s->last_launch, hipEventDisableTiming));
+        HIPCHECK(hipEventRecord(s->last_launch, st));
+        s->last_launch_valid = true;
         s->last_variant = -1;
         s->samples += p.n_items * (unsigned long long)frame_count;
         s->tests_per_seg = (unsigned long long)s->n_tris;
@@ -2355,6 +2436,37 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
         p.frame_split = 1;
         p.frame_buf = s->d_fb;
         p.n_items = p.n_pix * frame_count;
+    }
+    // cost-ordered items: the previous launch's per-pixel costs (same slab)
+    // give this launch's pixel order, most expensive first (a shorter tail)
+    if (s->cost_order) {
+        if (s->cost_cap < p.n_pix) {
+            (void)hipFree(s->d_cost);
+            (void)hipFree(s->d_order);
+            s->d_cost = s->d_order = nullptr;
+            s->cost_cap = 0;
+            s->cost_npix = 0;
+            HIPCHECK(hipMalloc(&s->d_cost, p.n_pix * sizeof(uint32_t)));
+            HIPCHECK(hipMalloc(&s->d_order, p.n_pix * sizeof(uint32_t)));
+            if (!s->d_hist) HIPCHECK(hipMalloc(&s->d_hist, 32 * sizeof(uint32_t)));
+            s->cost_cap = p.n_pix;
+        }
+        const int key[4] = {(int)u->width, sh.tile_rows, sh.rank, sh.nranks};
+        const bool valid = s->cost_npix == p.n_pix && std::memcmp(key, s->cost_key, sizeof(key)) == 0;
+        const unsigned long long runs = p.n_pix / 64;
+        if (valid && runs > 0) {
+            const unsigned blocks = (unsigned)std::min<unsigned long long>((runs + 255) / 256, 2048);
+            HIPCHECK(hipMemsetAsync(s->d_hist, 0, 32 * sizeof(uint32_t), st));
+            hipLaunchKernelGGL(cost_histogram, dim3(blocks), dim3(256), 0, st, s->d_cost, runs, s->d_hist);
+            hipLaunchKernelGGL(cost_offsets, dim3(1), dim3(64), 0, st, s->d_hist);
+            hipLaunchKernelGGL(cost_scatter, dim3(blocks), dim3(256), 0, st, s->d_cost, runs, s->d_hist, s->d_order);
+            HIPCHECK(hipGetLastError());
+            p.order = s->d_order;
+            p.n_runs = (uint32_t)runs;
+        }
+        p.cost_out = s->d_cost;
+        s->cost_npix = p.n_pix;
+        std::memcpy(s->cost_key, key, sizeof(key));
     }
     const size_t resident_bytes = (size_t)3 * sizeof(float4) * (size_t)std::max(s->n_tris, 1);
     const bool fits = resident_bytes <= kResidentMaxBytes;
@@ -2395,6 +2507,9 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
                            p.n_pix, frame_count, p.accum, p.accum8);
         HIPCHECK(hipGetLastError());
     }
+    if (!s->last_launch) HIPCHECK(hipEventCreateWithFlags(&s->last_launch, hipEventDisableTiming));
+    HIPCHECK(hipEventRecord(s->last_launch, st));
+    s->last_launch_valid = true;
     s->samples += p.n_pix * (unsigned long long)p.R * (unsigned long long)frame_count;
     s->tests_per_seg = (unsigned long long)s->n_tris;
     return 0;

@@ -155,7 +155,7 @@ assert TRI_DTYPE.itemsize == 80 and MAT_DTYPE.itemsize == 96 and NODE_DTYPE.item
 EXPORTED = [
     "rt2_last_error", "rt2_abi_version", "rt2_scene_create", "rt2_scene_destroy", "rt2_shard_rows",
     "rt2_shard_row", "rt2_render", "rt2_render_host", "rt2_resolve_rgba32f", "rt2_resolve_rgb8_reference",
-    "rt2_scene_stats", "rt2_scene_set_variant", "rt2_scene_set_traversal", "rt2_scene_set_frame_split", "rt2_sd_create", "rt2_sd_destroy", "rt2_sd_load_obj_folder",
+    "rt2_scene_stats", "rt2_scene_set_variant", "rt2_scene_set_traversal", "rt2_scene_set_frame_split", "rt2_scene_set_cost_order", "rt2_sd_create", "rt2_sd_destroy", "rt2_sd_load_obj_folder",
     "rt2_sd_add_material", "rt2_sd_add_triangle", "rt2_sd_add_triangles", "rt2_sd_add_cornell_box", "rt2_sd_add_mirror_cornell_box",
     "rt2_sd_add_side_lit_cornell_box", "rt2_sd_add_sky_light_plane", "rt2_sd_add_cube",
     "rt2_sd_create_classic_cornell_box", "rt2_sd_create_diverse_cornell_box", "rt2_sd_build_bvh",
@@ -210,6 +210,7 @@ def lib() -> C.CDLL:
         "rt2_scene_set_variant": (C.c_int, [P, C.c_int]),
         "rt2_scene_set_traversal": (C.c_int, [P, C.c_int]),
         "rt2_scene_set_frame_split": (C.c_int, [P, C.c_int]),
+        "rt2_scene_set_cost_order": (C.c_int, [P, C.c_int]),
         "rt2_scene_set_textures": (C.c_int, [P, C.POINTER(Image), I32]),
         "rt2_image_load": (C.c_int, [C.c_char_p, I32, C.POINTER(Image)]),
         "rt2_image_free": (None, [C.POINTER(Image)]),
@@ -466,6 +467,10 @@ class Scene:
     def set_frame_split(self, enable: bool) -> None:
         """(frame, pixel) work items for multi-frame renders (rt2_scene_set_frame_split)."""
         _check(lib().rt2_scene_set_frame_split(self._p, int(bool(enable))), "set_frame_split")
+
+    def set_cost_order(self, enable: bool) -> None:
+        """Most-expensive-first pixel order from the previous render (rt2_scene_set_cost_order)."""
+        _check(lib().rt2_scene_set_cost_order(self._p, int(bool(enable))), "set_cost_order")
 
     def set_textures(self, images) -> None:
         """Uploads textures (list of (h, w, channels) uint8 arrays, stb layout) — the

@@ -24,6 +24,7 @@ ap.add_argument("--rays", type=int, default=0)
 ap.add_argument("--frames", type=int, default=0)
 ap.add_argument("--traversal", default="brute", choices=["brute", "bvh"])
 ap.add_argument("--no-split", action="store_true", help="whole-pixel items for F > 1")
+ap.add_argument("--cost-order", type=int, default=-1, help="1/0: force most-expensive-first item order on/off")
 a = ap.parse_args()
 sd, spec = rt2.build_config_scene(a.config)
 W, H, R = a.width or spec.width, a.height or spec.height, a.rays or spec.rays
@@ -31,6 +32,8 @@ u = rt2.offline_uniforms(W, H, spec.bounces, R, sd.num_triangles)
 scene = rt2.Scene(sd, 0)
 scene.set_traversal(a.traversal)
 scene.set_frame_split(not a.no_split)
+if a.cost_order >= 0:
+    scene.set_cost_order(bool(a.cost_order))
 F = a.frames or spec.frames
 variants = [int(v) for v in a.variants.split(",")]
 times = {v: [] for v in variants}
@@ -70,5 +73,6 @@ for v in variants:
     med = float(np.median(times[v]))
     out[rt2.lib().rt2_variant_name(v).decode()] = dict(variant=v, median_ms=round(med * 1e3, 2),
                                                         min_ms=round(min(times[v]) * 1e3, 2),
+                                                        all_ms=[round(t * 1e3, 1) for t in times[v]],
                                                         msamples_s=round(samples / med / 1e6, 2))
 print(json.dumps({"config": a.config, "W": W, "H": H, "R": R, "variants": out, "diag": diag}, indent=1))

@@ -289,3 +289,27 @@ def test_team_tail_small_slab(rt2mod, oraclemod, config_scene, torch_cuda, varia
     rows = rt2mod.shard_row_ids(H, sh)
     ref, _, _ = oracle_mean(oraclemod, sd, u, rows, 0, 1)
     assert_exact(img, ref, f"team variant {variant} slab")
+
+
+@pytest.mark.parametrize("traversal,frames", [("brute", 1), ("bvh", 1), ("brute", 3), ("bvh", 2)])
+def test_cost_ordered_renders_identical(rt2mod, oraclemod, config_scene, torch_cuda, traversal, frames):
+    """Renders after the first hand out pixels most-expensive-first (the previous
+    render's cost map): same bits, every pixel exactly once."""
+    sd, spec = config_scene("B")
+    W, H = 120, 66
+    u = rt2mod.offline_uniforms(W, H, spec.bounces, 4, sd.num_triangles)
+    scene = rt2mod.Scene(sd, 0)
+    scene.set_traversal(traversal)
+    scene.set_cost_order(True)
+    imgs = [scene.render_host(u, 0, frames, rgb8=True) for _ in range(3)]
+    st = scene.stats(reset=True)
+    assert st.samples == 3 * W * H * 4 * frames
+    for img, img8 in imgs[1:]:
+        assert np.array_equal(img, imgs[0][0]) and np.array_equal(img8, imgs[0][1])
+    ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(H), 0, frames, traversal)
+    assert_exact(imgs[2][0], ref, f"cost-ordered {traversal} F={frames}")
+    # a different slab invalidates the map (no stale order is applied)
+    sh = rt2mod.shard(2, 1, 3)
+    img = scene.render_host(u, 0, frames, sh)
+    rows = rt2mod.shard_row_ids(H, sh)
+    assert np.array_equal(img, imgs[0][0][rows])
