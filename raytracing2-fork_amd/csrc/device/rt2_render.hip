@@ -1886,6 +1886,7 @@ struct rt2_scene {
     int bvh_root = 0;                           // BVH v2 stack entry of node 0
     int recs_ok = 0;                            // BVH v3 fast-path precondition on the boxes
     int split_frames = 1;                       // frame-major (frame, pixel) items when F > 1
+    unsigned long long frame_scratch_cap = 2ull << 30;  // bytes of per-frame planes per launch
     int cost_order = 0;                         // order items by the previous launch's per-pixel cost (opt-in)
     uint32_t* d_cost = nullptr;                 // per-pixel cost map of the last launch
     uint32_t* d_order = nullptr;                // pixel order for the next launch
@@ -2048,6 +2049,13 @@ extern "C" int rt2_scene_set_textures(rt2_scene* s, const rt2_image* images, int
     HIPCHECK(hipMemcpy(s->d_texels, host.data(), total * sizeof(uchar4), hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(s->d_tex_desc, desc.data(), n * sizeof(int4), hipMemcpyHostToDevice));
     s->n_tex = n;
+    return 0;
+}
+
+// Not in rt2.h (test hook): bytes of per-frame colour planes one launch may use.
+extern "C" int rt2_scene_set_frame_scratch_cap(rt2_scene* s, unsigned long long bytes) {
+    if (!s || bytes == 0) return -1;
+    s->frame_scratch_cap = bytes;
     return 0;
 }
 
@@ -2339,6 +2347,22 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
         return -1;
     }
     if (frame_count == 0 || rows == 0) return 0;
+    // frame-major items keep one colour plane per frame: beyond frame_scratch_cap
+    // of planes (or 2^32 items), render consecutive frame chunks — the
+    // accumulation stays in frame order, so the sums are unchanged
+    if (!u->basicShading && s->split_frames && frame_count > 1) {
+        const unsigned long long npix = (unsigned long long)rows * u->width;
+        unsigned long long chunk = std::max<unsigned long long>(1, s->frame_scratch_cap / (npix * sizeof(float4)));
+        chunk = std::min<unsigned long long>(chunk, 0xfffffffeull / std::max<unsigned long long>(npix, 1));
+        if (chunk < frame_count) {
+            for (unsigned long long f0 = 0; f0 < frame_count; f0 += chunk) {
+                const uint32_t fc = (uint32_t)std::min<unsigned long long>(chunk, frame_count - f0);
+                const int rc = rt2_render(s, u, frame_begin + (uint32_t)f0, fc, sh, d_accum, d_accum8, stream);
+                if (rc != 0) return rc;
+            }
+            return 0;
+        }
+    }
     HIPCHECK(hipSetDevice(s->device));
     hipStream_t st = (hipStream_t)stream;
 

@@ -313,3 +313,21 @@ def test_cost_ordered_renders_identical(rt2mod, oraclemod, config_scene, torch_c
     img = scene.render_host(u, 0, frames, sh)
     rows = rt2mod.shard_row_ids(H, sh)
     assert np.array_equal(img, imgs[0][0][rows])
+
+
+def test_frame_chunks_identical(rt2mod, config_scene, torch_cuda):
+    """Per-frame planes beyond the scratch cap: the frames render in chunks,
+    accumulated in order — the same bits as one launch."""
+    import ctypes as C
+    sd, spec = config_scene("B")
+    W, H, F = 64, 40, 5
+    u = rt2mod.offline_uniforms(W, H, spec.bounces, 2, sd.num_triangles)
+    a = rt2mod.Scene(sd, 0)
+    ref = a.render_host(u, 1, F, rgb8=True)
+    b = rt2mod.Scene(sd, 0)
+    L = rt2mod.lib()
+    L.rt2_scene_set_frame_scratch_cap.argtypes = [C.c_void_p, C.c_ulonglong]
+    assert L.rt2_scene_set_frame_scratch_cap(b._p, W * H * 16 * 2) == 0  # two frames per chunk
+    got = b.render_host(u, 1, F, rgb8=True)
+    assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1])
+    assert b.stats().samples == W * H * 2 * F
