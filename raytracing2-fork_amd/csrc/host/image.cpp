@@ -30,17 +30,25 @@ struct Fail : std::runtime_error {
 };
 [[noreturn]] void fail(const std::string& m) { throw Fail(m); }
 
+// int arithmetic that wraps (as stb's C int arithmetic does on this
+// compiler) instead of overflowing: only corrupt streams get near the limits
+inline int wadd(int a, int b) { return (int)((uint32_t)a + (uint32_t)b); }
+inline int wsub(int a, int b) { return (int)((uint32_t)a - (uint32_t)b); }
+inline int wmul(int a, int b) { return (int)((uint32_t)a * (uint32_t)b); }
+
 uint32_t be32(const uint8_t* p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
 uint16_t be16(const uint8_t* p) { return (uint16_t)(p[0] << 8 | p[1]); }
 
-constexpr int kMaxDim = 1 << 24;  // STBI_MAX_DIMENSIONS
+constexpr int kMaxDim = 1 << 24;                    // STBI_MAX_DIMENSIONS
+constexpr unsigned long long kMaxBytes = 1ull << 31;  // decoded-size limit (stb's int-sized allocations)
 
 // ----------------------------------------------------------------------------
 // PNG
 // ----------------------------------------------------------------------------
 
 std::vector<uint8_t> zlib_inflate(const std::vector<uint8_t>& in, size_t guess) {
-    std::vector<uint8_t> out(std::max<size_t>(guess, 1024));
+    // the guess comes from the (untrusted) header: start small, grow with the data
+    std::vector<uint8_t> out(std::min<size_t>(std::max<size_t>(guess, 1024), 1u << 24));
     z_stream zs;
     std::memset(&zs, 0, sizeof(zs));
     if (inflateInit(&zs) != Z_OK) fail("zlib init");
@@ -58,6 +66,10 @@ std::vector<uint8_t> zlib_inflate(const std::vector<uint8_t>& in, size_t guess) 
             fail("Corrupt PNG (zlib stream)");
         }
         if (zs.avail_out == 0) {
+            if (out.size() >= kMaxBytes) {
+                inflateEnd(&zs);
+                fail("Corrupt PNG (image data too large)");
+            }
             out.resize(out.size() * 2);
         } else if (zs.avail_in == 0) {
             inflateEnd(&zs);
@@ -173,7 +185,7 @@ Image decode_png(const std::vector<uint8_t>& d) {
                 has_trans = true;
                 for (int k = 0; k < img_n; k++) {
                     tc16[k] = be16(c + 2 * k);
-                    tc8[k] = (uint8_t)((tc16[k] & 255) * depth_scale[depth]);
+                    if (depth < 16) tc8[k] = (uint8_t)((tc16[k] & 255) * depth_scale[depth]);
                 }
             }
         } else if (is("IDAT")) {
@@ -187,6 +199,7 @@ Image decode_png(const std::vector<uint8_t>& d) {
         pos += 12 + (size_t)len;
     }
     if (idat.empty()) fail("Corrupt PNG (no IDAT)");
+    if ((unsigned long long)w * h * (img_n + 1) * (depth == 16 ? 2 : 1) > kMaxBytes) fail("PNG too large");
     const std::vector<uint8_t> raw = zlib_inflate(idat, ((size_t)w * depth * img_n + 15) / 8 * h + h);
 
     // samples at the file's depth: 8-bit (scaled low depths) or 16-bit
@@ -427,6 +440,7 @@ void JpegDecoder::read_sof(int len) {
     if (h_ == 0) fail("JPEG format not supported: delayed height");
     if (w_ == 0) fail("Corrupt JPEG (0 width)");
     if (h_ > kMaxDim || w_ > kMaxDim) fail("Very large image (corrupt?)");
+    if ((unsigned long long)w_ * h_ * 4 > kMaxBytes) fail("JPEG too large");
     const int nc = byte();
     if (nc != 1 && nc != 3) fail("JPEG: only 1 or 3 components are supported");
     if (len != 8 + 3 * nc) fail("Corrupt JPEG (bad SOF len)");
@@ -511,7 +525,7 @@ void JpegDecoder::block(JComp& c, int16_t data[64]) {
         } else {
             k += r;
             const int zig = kDezigzag[k++];
-            data[zig] = (int16_t)(extend(getbits(s), s) * dq[zig]);
+            data[zig] = (int16_t)wmul(extend(getbits(s), s), dq[zig]);
         }
     } while (k < 64);
 }
@@ -525,31 +539,31 @@ struct Idct1D {
     int t0, t1, t2, t3, x0, x1, x2, x3;
     void run(int s0, int s1, int s2, int s3, int s4, int s5, int s6, int s7) {
         // even part
-        const int p1 = (s2 + s6) * fix12(0.5411961f);
-        const int e2 = p1 + s6 * fix12(-1.847759065f);
-        const int e3 = p1 + s2 * fix12(0.765366865f);
-        const int e0 = (s0 + s4) * 4096;
-        const int e1 = (s0 - s4) * 4096;
-        x0 = e0 + e3;
-        x3 = e0 - e3;
-        x1 = e1 + e2;
-        x2 = e1 - e2;
+        const int p1 = wmul(wadd(s2, s6), fix12(0.5411961f));
+        const int e2 = wadd(p1, wmul(s6, fix12(-1.847759065f)));
+        const int e3 = wadd(p1, wmul(s2, fix12(0.765366865f)));
+        const int e0 = wmul(wadd(s0, s4), 4096);
+        const int e1 = wmul(wsub(s0, s4), 4096);
+        x0 = wadd(e0, e3);
+        x3 = wsub(e0, e3);
+        x1 = wadd(e1, e2);
+        x2 = wsub(e1, e2);
         // odd part (s7, s5, s3, s1)
         int o0 = s7, o1 = s5, o2 = s3, o3 = s1;
-        int q3 = o0 + o2, q4 = o1 + o3, q1 = o0 + o3, q2 = o1 + o2;
-        const int q5 = (q3 + q4) * fix12(1.175875602f);
-        o0 = o0 * fix12(0.298631336f);
-        o1 = o1 * fix12(2.053119869f);
-        o2 = o2 * fix12(3.072711026f);
-        o3 = o3 * fix12(1.501321110f);
-        q1 = q5 + q1 * fix12(-0.899976223f);
-        q2 = q5 + q2 * fix12(-2.562915447f);
-        q3 = q3 * fix12(-1.961570560f);
-        q4 = q4 * fix12(-0.390180644f);
-        t3 = o3 + q1 + q4;
-        t2 = o2 + q2 + q3;
-        t1 = o1 + q2 + q4;
-        t0 = o0 + q1 + q3;
+        int q3 = wadd(o0, o2), q4 = wadd(o1, o3), q1 = wadd(o0, o3), q2 = wadd(o1, o2);
+        const int q5 = wmul(wadd(q3, q4), fix12(1.175875602f));
+        o0 = wmul(o0, fix12(0.298631336f));
+        o1 = wmul(o1, fix12(2.053119869f));
+        o2 = wmul(o2, fix12(3.072711026f));
+        o3 = wmul(o3, fix12(1.501321110f));
+        q1 = wadd(q5, wmul(q1, fix12(-0.899976223f)));
+        q2 = wadd(q5, wmul(q2, fix12(-2.562915447f)));
+        q3 = wmul(q3, fix12(-1.961570560f));
+        q4 = wmul(q4, fix12(-0.390180644f));
+        t3 = wadd(wadd(o3, q1), q4);
+        t2 = wadd(wadd(o2, q2), q3);
+        t1 = wadd(wadd(o1, q2), q4);
+        t0 = wadd(wadd(o0, q1), q3);
     }
 };
 
@@ -561,15 +575,15 @@ void idct_islow(const int16_t in[64], uint8_t* out, int stride) {
         const int16_t* d = in + i;
         Idct1D t;
         t.run(d[0], d[8], d[16], d[24], d[32], d[40], d[48], d[56]);
-        const int x0 = t.x0 + 512, x1 = t.x1 + 512, x2 = t.x2 + 512, x3 = t.x3 + 512;
-        v[i + 0] = (x0 + t.t3) >> 10;
-        v[i + 56] = (x0 - t.t3) >> 10;
-        v[i + 8] = (x1 + t.t2) >> 10;
-        v[i + 48] = (x1 - t.t2) >> 10;
-        v[i + 16] = (x2 + t.t1) >> 10;
-        v[i + 40] = (x2 - t.t1) >> 10;
-        v[i + 24] = (x3 + t.t0) >> 10;
-        v[i + 32] = (x3 - t.t0) >> 10;
+        const int x0 = wadd(t.x0, 512), x1 = wadd(t.x1, 512), x2 = wadd(t.x2, 512), x3 = wadd(t.x3, 512);
+        v[i + 0] = wadd(x0, t.t3) >> 10;
+        v[i + 56] = wsub(x0, t.t3) >> 10;
+        v[i + 8] = wadd(x1, t.t2) >> 10;
+        v[i + 48] = wsub(x1, t.t2) >> 10;
+        v[i + 16] = wadd(x2, t.t1) >> 10;
+        v[i + 40] = wsub(x2, t.t1) >> 10;
+        v[i + 24] = wadd(x3, t.t0) >> 10;
+        v[i + 32] = wsub(x3, t.t0) >> 10;
     }
     for (int r = 0; r < 8; r++) {
         const int* s = v + 8 * r;
@@ -577,15 +591,15 @@ void idct_islow(const int16_t in[64], uint8_t* out, int stride) {
         Idct1D t;
         t.run(s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7]);
         const int bias = 65536 + (128 << 17);
-        const int x0 = t.x0 + bias, x1 = t.x1 + bias, x2 = t.x2 + bias, x3 = t.x3 + bias;
-        o[0] = clamp8((x0 + t.t3) >> 17);
-        o[7] = clamp8((x0 - t.t3) >> 17);
-        o[1] = clamp8((x1 + t.t2) >> 17);
-        o[6] = clamp8((x1 - t.t2) >> 17);
-        o[2] = clamp8((x2 + t.t1) >> 17);
-        o[5] = clamp8((x2 - t.t1) >> 17);
-        o[3] = clamp8((x3 + t.t0) >> 17);
-        o[4] = clamp8((x3 - t.t0) >> 17);
+        const int x0 = wadd(t.x0, bias), x1 = wadd(t.x1, bias), x2 = wadd(t.x2, bias), x3 = wadd(t.x3, bias);
+        o[0] = clamp8(wadd(x0, t.t3) >> 17);
+        o[7] = clamp8(wsub(x0, t.t3) >> 17);
+        o[1] = clamp8(wadd(x1, t.t2) >> 17);
+        o[6] = clamp8(wsub(x1, t.t2) >> 17);
+        o[2] = clamp8(wadd(x2, t.t1) >> 17);
+        o[5] = clamp8(wsub(x2, t.t1) >> 17);
+        o[3] = clamp8(wadd(x3, t.t0) >> 17);
+        o[4] = clamp8(wsub(x3, t.t0) >> 17);
     }
 }
 
