@@ -1,0 +1,177 @@
+// Brute-force render kernels: RESIDENT, TILED and SMEM (north-star path).
+// Included by rt2_render.hip only (one translation unit; internal linkage).
+#pragma once
+
+namespace {
+
+// RESIDENT: all triangles in LDS, waves independent after the initial load.
+template <int BLOCK, int MT, int UNROLL>
+__global__ __launch_bounds__(BLOCK) void render_resident(RenderParams p) {
+    // UNROLL == 0 on a grouped variant = diagnostic build with sweep counters
+    constexpr bool kStats = MT >= 2 && UNROLL == 0;
+    SweepStats ss;
+    extern __shared__ float4 lds[];
+    const int n4 = 3 * p.n_tris;
+    for (int i = threadIdx.x; i < n4; i += BLOCK) lds[i] = p.tri[i];
+    __syncthreads();
+
+    Lane L;
+    lane_init(L);
+    for (;;) {
+        advance(L, p);
+        if (!__any(L.st == ST_TRACE)) break;
+        if (L.st == ST_TRACE) {
+            L.bounce += 1;
+            L.segs += 1;
+            float best = 1e38f, bestK = 1e38f * 1.0009765625f;
+            int bi = -1;
+            const f3 o = L.o, d = L.d;
+            if constexpr (MT >= 200) {
+                sweep_lean<MT - 200, false>(o, d, lds, nullptr, p.n_tris, 0, best, bi, bestK);
+            } else if constexpr (MT >= 100) {
+                sweep_masked<MT - 100, false>(o, d, lds, nullptr, p.n_tris, 0, best, bi, bestK);
+            } else if constexpr (MT >= 2) {
+                sweep_grouped<MT, kStats>(o, d, lds, p.n_tris, 0, best, bi, bestK, &ss);
+            } else {
+#pragma unroll UNROLL
+                for (int i = 0; i < p.n_tris; i++) {
+                    mt_dispatch<MT>(o, d, lds[3 * i], lds[3 * i + 1], lds[3 * i + 2], i, best, bi, bestK);
+                }
+            }
+            shade(L, p, best, bi);
+        }
+    }
+    flush_counters(L, p);
+    if constexpr (kStats) {
+        unsigned long long surv = ss.lane_survivors;
+        for (int off = 32; off > 0; off >>= 1) surv += __shfl_xor(surv, off);
+        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+        if (lane_id() == 0) {
+            atomicAdd(p.seg_counter + 1, (unsigned long long)ss.groups);
+            atomicAdd(p.seg_counter + 2, (unsigned long long)ss.groups_exact);
+            atomicAdd(p.seg_counter + 3, (unsigned long long)ss.exact_iters);
+            atomicAdd(p.seg_counter + 4, surv);
+            // wave finish-time spread: [6] = earliest wave end, [5] = latest (ticks of 10 ns)
+            atomicMin(p.seg_counter + 5, t_end);
+            atomicMax(p.seg_counter + 4 + 2, t_end);
+        }
+    }
+}
+
+// TILED: triangles streamed through LDS; the workgroup sweeps in lockstep.
+template <int BLOCK, int MT, int UNROLL>
+__global__ __launch_bounds__(BLOCK) void render_tiled(RenderParams p) {
+    extern __shared__ float4 lds[];
+    __shared__ int block_any;
+    Lane L;
+    lane_init(L);
+    const int T = p.tile_tris;
+    for (;;) {
+        advance(L, p);
+        if (threadIdx.x == 0) block_any = 0;
+        __syncthreads();
+        if (L.st == ST_TRACE) block_any = 1;
+        __syncthreads();
+        if (!block_any) break;
+        const bool tracing = L.st == ST_TRACE;
+        float best = 1e38f, bestK = 1e38f * 1.0009765625f;
+        int bi = -1;
+        const f3 o = L.o, d = L.d;
+        for (int base = 0; base < p.n_tris; base += T) {
+            const int cnt = min(T, p.n_tris - base);
+            __syncthreads();
+            for (int i = threadIdx.x; i < 3 * cnt; i += BLOCK) lds[i] = p.tri[3 * base + i];
+            __syncthreads();
+            if (tracing) {
+                if constexpr (MT >= 100) {
+                    sweep_masked<MT - 100, false>(o, d, lds, nullptr, cnt, base, best, bi, bestK);
+                } else if constexpr (MT >= 2) {
+                    sweep_grouped<MT>(o, d, lds, cnt, base, best, bi, bestK);
+                } else {
+#pragma unroll UNROLL
+                    for (int i = 0; i < cnt; i++)
+                        mt_dispatch<MT>(o, d, lds[3 * i], lds[3 * i + 1], lds[3 * i + 2], base + i, best, bi, bestK);
+                }
+            }
+        }
+        if (tracing) {
+            L.bounce += 1;
+            L.segs += 1;
+            shade(L, p, best, bi);
+        }
+    }
+    flush_counters(L, p);
+}
+
+// SMEM: no LDS; triangles reach the VALU through the scalar cache (sweep_smem).
+// COOP > 0: drain mode — once the item pool is exhausted (some lane is DONE)
+// and at most COOP lanes of the wave still trace, each live ray's closest hit
+// is computed by the whole wave (coop_closest), one ray at a time.
+template <int BLOCK, int G, int COOP, int WPE>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void render_smem(RenderParams p) {
+    cfloat* tri = (cfloat*)p.tri;
+    Lane L;
+    lane_init(L);
+    for (;;) {
+        advance(L, p);
+        const unsigned long long act = __ballot(L.st == ST_TRACE);
+        if (!act) break;
+        if (COOP >= 100 && __popcll(act) <= (unsigned)(COOP - 100) && __any(L.st == ST_DONE)) {
+            float b;
+            int bidx;
+            team_closest(L.o, L.d, p.tri, p.n_tris, act, b, bidx);
+            if (L.st == ST_TRACE) {
+                L.bounce += 1;
+                L.segs += 1;
+                shade(L, p, b, bidx);
+            }
+            continue;
+        }
+        if (COOP > 0 && COOP < 100 && __popcll(act) <= (unsigned)COOP && __any(L.st == ST_DONE)) {
+            float mybest = 1e38f;
+            int mybi = -1;
+            unsigned long long m = act;
+            while (m) {
+                const int j = __builtin_ctzll(m);
+                m &= m - 1;
+                const f3 oj = mk(__shfl(L.o.x, j), __shfl(L.o.y, j), __shfl(L.o.z, j));
+                const f3 dj = mk(__shfl(L.d.x, j), __shfl(L.d.y, j), __shfl(L.d.z, j));
+                float b;
+                int bidx;
+                coop_closest(oj, dj, p.tri, p.n_tris, b, bidx);
+                if ((int)lane_id() == j) {
+                    mybest = b;
+                    mybi = bidx;
+                }
+            }
+            if (L.st == ST_TRACE) {
+                L.bounce += 1;
+                L.segs += 1;
+                shade(L, p, mybest, mybi);
+            }
+            continue;
+        }
+        if (L.st == ST_TRACE) {
+            L.bounce += 1;
+            L.segs += 1;
+            float best = 1e38f, bestK = 1e38f * 1.0009765625f;
+            int bi = -1;
+            const f3 o = L.o, d = L.d;
+            if constexpr (G >= 400)
+                sweep_minfilter<G - 400>(o, d, (const float*)p.tri, p.n_tris, best, bi, bestK);
+            else if constexpr (G >= 300)
+                sweep_ballot<G - 300>(o, d, (const float*)p.tri, p.n_tris, best, bi, bestK);
+            else if constexpr (G >= 200)
+                sweep_lean<G - 200, true>(o, d, nullptr, (const float*)p.tri, p.n_tris, 0, best, bi, bestK);
+            else if constexpr (G >= 100)
+                sweep_masked<G - 100, true>(o, d, nullptr, p.tri ? (const float*)p.tri : nullptr, p.n_tris, 0, best,
+                                            bi, bestK);
+            else
+                sweep_smem<G>(o, d, tri, p.n_tris, best, bi, bestK);
+            shade(L, p, best, bi);
+        }
+    }
+    flush_counters(L, p);
+}
+
+}  // namespace
