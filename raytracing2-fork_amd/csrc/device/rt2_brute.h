@@ -157,7 +157,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             float best = 1e38f, bestK = 1e38f * 1.0009765625f;
             int bi = -1;
             const f3 o = L.o, d = L.d;
-            if constexpr (G >= 400)
+            if constexpr (G >= 500)
+                sweep_masked<G - 500, true, 1>(o, d, nullptr, (const float*)p.tri, p.n_tris, 0, best, bi, bestK);
+            else if constexpr (G >= 400)
                 sweep_minfilter<G - 400>(o, d, (const float*)p.tri, p.n_tris, best, bi, bestK);
             else if constexpr (G >= 300)
                 sweep_ballot<G - 300>(o, d, (const float*)p.tri, p.n_tris, best, bi, bestK);

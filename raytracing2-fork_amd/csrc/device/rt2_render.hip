@@ -508,6 +508,9 @@ const Variant kVariants[] = {
     RT2_VARIANT(K_SMEM, 256, 132108, 1, "smem/256/masked8/team32"),  // 64
     RT2_VARIANT(K_SMEM, 256, 148108, 1, "smem/256/masked8/team48"),  // 65
     RT2_VARIANT(K_SMEM, 256, 164108, 1, "smem/256/masked8/team64"),  // 66
+    RT2_VARIANT(K_SMEM, 256, 32508, 1, "smem/256/max3f8/coop32"),    // 67
+    RT2_VARIANT(K_SMEM, 256, 32504, 1, "smem/256/max3f4/coop32"),    // 68
+    RT2_VARIANT(K_SMEM, 256, 32508, 6, "smem/256/max3f8/coop32/w6"), // 69
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr size_t kResidentMaxBytes = 112 * 1024;

@@ -247,6 +247,30 @@ __device__ __forceinline__ bool mt_pass(const MtQ& q, float bestK) {
     return (q.tnum > 0.0f) & (q.U <= B) & (q.V >= -B) & ((q.V - q.U) <= q.det * 1.0009765625f) &
            (q.tnum <= q.det * bestK);
 }
+// mt_pass in 7 VALU instead of 9 and one compare (one lane mask, no SALU
+// and-chain): with B = det*2^-60 it passes iff
+//   max(U, -V, RN(V-U) - det*(1+2^-10), -tnum, tnum - det*bestK) <= B,
+// the two fused differences rounded once (their sign is exact).  Each term
+// above B rejects only what mt_pass's proof rejects ("Exactness of
+// the filter"): U > B and -V > B as before; RN(V-U) > det*(1+2^-10) exactly is
+// the w test with a tighter right side; -tnum > B >= 0 gives dst < 0;
+// tnum > det*bestK + B exactly gives dst >= best.  For det <= 0 (B <= 0) every
+// outcome is rejected by the exact test anyway.  A NaN term is ignored by
+// fmaxf (maxNum), which can only pass more.
+__device__ __forceinline__ bool mt_pass3(const MtQ& q, float bestK) {
+    const float B = q.det * 0x1p-60f;
+    const float X = __builtin_fmaf(-q.det, 1.0009765625f, q.V - q.U);
+    const float Y = __builtin_fmaf(-q.det, bestK, q.tnum);
+    return fmaxf(fmaxf(fmaxf(q.U, -q.V), X), fmaxf(-q.tnum, Y)) <= B;
+}
+template <int FILT>
+__device__ __forceinline__ bool mt_pass_f(const MtQ& q, float bestK) {
+    if constexpr (FILT == 1)
+        return mt_pass3(q, bestK);
+    else
+        return mt_pass(q, bestK);
+}
+
 // compute.glsl:312-327 on the phase-1 intermediates (exactly the reference arithmetic).
 __device__ __forceinline__ void mt_exact(const MtQ& q, int idx, float& best, int& bi, float& bestK) {
     if (!((q.det < 1e-10f && q.det > -1e-10f) || q.det < 0.0f)) {
@@ -267,7 +291,7 @@ __device__ __forceinline__ void mt_exact(const MtQ& q, int idx, float& best, int
 // per-lane bit packing); phase 2 runs mt_exact under each mask in index order
 // (skipped by a scalar branch when the mask is empty).  SMEM selects the
 // scalar-load path for the triangle records instead of LDS.
-template <int G, bool SMEM>
+template <int G, bool SMEM, int FILT = 0>
 __device__ __forceinline__ void sweep_masked(const f3& o, const f3& d, const float4* lds, const float* gtri,
                                              int count, int base, float& best, int& bi, float& bestK) {
     int i = 0;
@@ -289,7 +313,7 @@ __device__ __forceinline__ void sweep_masked(const f3& o, const f3& d, const flo
                 t2 = t[2];
             }
             q[k] = mt_quantities(o, d, t0, t1, t2);
-            f[k] = mt_pass(q[k], bestK);
+            f[k] = mt_pass_f<FILT>(q[k], bestK);
         }
 #pragma unroll
         for (int k = 0; k < G; k++)
@@ -309,7 +333,7 @@ __device__ __forceinline__ void sweep_masked(const f3& o, const f3& d, const flo
             t2 = t[2];
         }
         const MtQ q = mt_quantities(o, d, t0, t1, t2);
-        if (mt_pass(q, bestK)) mt_exact(q, base + i, best, bi, bestK);
+        if (mt_pass_f<FILT>(q, bestK)) mt_exact(q, base + i, best, bi, bestK);
     }
 }
 

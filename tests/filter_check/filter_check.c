@@ -1,0 +1,136 @@
+/* Conservativeness check of the brute-force kernel's division-free filters
+ * (rt2_sweep.h mt_pass and mt_pass3) against the reference's Möller–Trumbore
+ * update decision (compute.glsl:302-340 + the strict `dst < best` of :432).
+ *
+ * A filter may pass pairs the exact test rejects (they just take the exact
+ * path) but must never reject a pair the exact test would accept.  The
+ * arithmetic restates the device forms in binary32 with explicit fmaf (built
+ * with -ffp-contract=off), over random and adversarial rays: rays through
+ * triangle edges and vertices nudged by a few ulps, grazing rays around the
+ * det = 1e-10 cut, `best` at and around the hit distance, coordinates over
+ * six decades.
+ *
+ *   filter_check <pairs> <seed>   ->  "pairs accepts violations_old violations_new pass_old pass_new"
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+typedef struct { float x, y, z; } f3;
+static f3 mk(float x, float y, float z) { f3 r = {x, y, z}; return r; }
+static f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+static float dot(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
+static f3 cross(f3 a, f3 b) {
+    return mk(fmaf(a.y, b.z, -(a.z * b.y)), fmaf(a.z, b.x, -(a.x * b.z)), fmaf(a.x, b.y, -(a.y * b.x)));
+}
+
+static uint64_t s_rng;
+static uint64_t next64(void) {
+    s_rng ^= s_rng << 13;
+    s_rng ^= s_rng >> 7;
+    s_rng ^= s_rng << 17;
+    return s_rng;
+}
+static float uni(void) { return (float)((next64() >> 40) * (1.0 / 16777216.0)); }  /* [0,1) */
+static float sym(void) { return 2.0f * uni() - 1.0f; }
+static float nudge(float x, int k) {
+    for (; k > 0; k--) x = nextafterf(x, INFINITY);
+    for (; k < 0; k++) x = nextafterf(x, -INFINITY);
+    return x;
+}
+static int ik(int span) { return (int)(next64() % (uint64_t)(2 * span + 1)) - span; }
+static f3 normalize(f3 v) {
+    const float l = sqrtf(dot(v, v));
+    return mk(v.x / l, v.y / l, v.z / l);
+}
+
+typedef struct { float det, tnum, U, V; } Q;
+
+static Q quantities(f3 o, f3 d, f3 a, f3 e0, f3 e1, f3 n) {
+    Q q;
+    q.det = -dot(d, n);
+    const f3 ao = sub(o, a);
+    q.tnum = dot(ao, n);
+    const f3 c = cross(d, ao);
+    q.U = dot(e1, c);
+    q.V = dot(e0, c);
+    return q;
+}
+static int exact_updates(Q q, float best) {
+    if ((q.det < 1e-10f && q.det > -1e-10f) || q.det < 0.0f) return 0;
+    const float inv = 1.0f / q.det;
+    const float dst = q.tnum * inv;
+    const float u = -q.U * inv;
+    const float v = q.V * inv;
+    return !(dst <= 1e-6f) && !(u < 0.0f || v < 0.0f || 1.0f - u - v < 0.0f) && dst < best;
+}
+static int pass_old(Q q, float bestK) {
+    const float B = q.det * 0x1p-60f;
+    return (q.tnum > 0.0f) & (q.U <= B) & (q.V >= -B) & ((q.V - q.U) <= q.det * 1.0009765625f) &
+           (q.tnum <= q.det * bestK);
+}
+static int pass_new(Q q, float bestK) {
+    const float B = q.det * 0x1p-60f;
+    const float X = fmaf(-q.det, 1.0009765625f, q.V - q.U);
+    const float Y = fmaf(-q.det, bestK, q.tnum);
+    return fmaxf(fmaxf(fmaxf(q.U, -q.V), X), fmaxf(-q.tnum, Y)) <= B;
+}
+
+int main(int argc, char** argv) {
+    const long long n = argc > 1 ? atoll(argv[1]) : 1000000;
+    s_rng = argc > 2 ? strtoull(argv[2], 0, 10) * 0x9E3779B97F4A7C15ull + 1 : 88172645463325252ull;
+    long long accepts = 0, bad_old = 0, bad_new = 0, p_old = 0, p_new = 0;
+    for (long long it = 0; it < n; it++) {
+        const int kind = (int)(next64() % 6);
+        const float scale = powf(10.0f, 4.0f * uni() - 2.0f);  /* 1e-2 .. 1e2 */
+        const float tsz = scale * powf(10.0f, -3.0f * uni());
+        const f3 c0 = mk(scale * sym(), scale * sym(), scale * sym());
+        const f3 a = c0;
+        const f3 b = mk(c0.x + tsz * sym(), c0.y + tsz * sym(), c0.z + tsz * sym());
+        const f3 c = mk(c0.x + tsz * sym(), c0.y + tsz * sym(), c0.z + tsz * sym());
+        const f3 e0 = sub(b, a), e1 = sub(c, a), nrm = cross(e0, e1);
+        /* aim point: inside, on an edge, at a vertex */
+        float wu = uni(), wv = uni();
+        if (wu + wv > 1.0f) { wu = 1.0f - wu; wv = 1.0f - wv; }
+        if (kind == 1) wu = 0.0f;
+        if (kind == 2) wv = 0.0f;
+        if (kind == 3) wv = 1.0f - wu;
+        if (kind == 4) { wu = (float)(next64() & 1); wv = wu > 0.0f ? 0.0f : (float)(next64() & 1); }
+        const f3 p = mk(a.x + wu * e0.x + wv * e1.x, a.y + wu * e0.y + wv * e1.y, a.z + wu * e0.z + wv * e1.z);
+        f3 o = mk(c0.x + 2.0f * scale * sym(), c0.y + 2.0f * scale * sym(), c0.z + 2.0f * scale * sym());
+        f3 d;
+        if (kind == 5) {
+            /* grazing: direction (nearly) in the triangle's plane */
+            const f3 t = normalize(e0);
+            const f3 nn = normalize(nrm);
+            const float eps = powf(10.0f, -12.0f * uni()) * (float)(next64() & 1 ? 1 : -1);
+            d = normalize(mk(t.x + eps * nn.x, t.y + eps * nn.y, t.z + eps * nn.z));
+            o = mk(p.x - 3.0f * scale * d.x, p.y - 3.0f * scale * d.y, p.z - 3.0f * scale * d.z);
+        } else {
+            d = normalize(sub(p, o));
+        }
+        d = mk(nudge(d.x, ik(2)), nudge(d.y, ik(2)), nudge(d.z, ik(2)));
+        o = mk(nudge(o.x, ik(3)), nudge(o.y, ik(3)), nudge(o.z, ik(3)));
+        const Q q = quantities(o, d, a, e0, e1, nrm);
+        float best;
+        const int bk = (int)(next64() % 4);
+        if (bk == 0) {
+            best = 1e38f;
+        } else {
+            const float dst = q.det != 0.0f ? q.tnum * (1.0f / q.det) : 1.0f;
+            best = bk == 1 ? nudge(fabsf(dst), ik(4)) : fabsf(dst) * (0.5f + uni());
+            if (!(best > 0.0f) || isinf(best) || isnan(best)) best = 1e38f;
+        }
+        const float bestK = best * 1.0009765625f;
+        const int ex = exact_updates(q, best);
+        const int fo = pass_old(q, bestK), fn = pass_new(q, bestK);
+        accepts += ex;
+        p_old += fo;
+        p_new += fn;
+        if (ex && !fo) bad_old++;
+        if (ex && !fn) bad_new++;
+    }
+    printf("%lld %lld %lld %lld %lld %lld\n", n, accepts, bad_old, bad_new, p_old, p_new);
+    return 0;
+}

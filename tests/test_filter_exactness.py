@@ -1,0 +1,50 @@
+"""The brute-force kernel's division-free filters never reject a pair the
+reference's Möller–Trumbore test accepts (CPU restatement of rt2_sweep.h
+mt_pass / mt_pass3 in binary32; proof in DESIGN.md, "Exactness of the
+filter").  tests/filter_check/filter_check.c draws random and adversarial
+rays (edges, vertices, grazing, best at the hit distance); a tightened
+filter mutant shows violations, so the harness is sensitive."""
+import os
+import subprocess
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "filter_check", "filter_check.c")
+
+
+@pytest.fixture(scope="module")
+def checker(tmp_path_factory):
+    exe = str(tmp_path_factory.mktemp("fc") / "filter_check")
+    subprocess.run(["gcc", "-O2", "-std=c11", "-ffp-contract=off", "-o", exe, SRC, "-lm"], check=True)
+    return exe
+
+
+def _run(exe, n, seed):
+    out = subprocess.run([exe, str(n), str(seed)], check=True, capture_output=True, text=True).stdout
+    pairs, accepts, bad_old, bad_new, p_old, p_new = map(int, out.split())
+    return pairs, accepts, bad_old, bad_new, p_old, p_new
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_filters_conservative(checker, seed):
+    pairs, accepts, bad_old, bad_new, p_old, p_new = _run(checker, 3_000_000, seed)
+    assert accepts > pairs // 20          # the adversarial draws do reach the accept region
+    assert bad_old == 0 and bad_new == 0  # no accepted pair is filtered out
+    assert p_new <= p_old * 1.01          # and the new form filters as much as the old one
+
+
+def test_harness_detects_a_wrong_filter(tmp_path):
+    src = open(SRC).read()
+    old = "return fmaxf(fmaxf(fmaxf(q.U, -q.V), X), fmaxf(-q.tnum, Y)) <= B;"
+    assert old in src
+    mutant = src.replace(old, "return fmaxf(fmaxf(fmaxf(q.U, -q.V), fmaf(-q.det, 1.0f, q.V - q.U)), "
+                              "fmaxf(-q.tnum, fmaf(-q.det, best_plain(bestK), q.tnum))) <= 0.0f;")
+    mutant = mutant.replace("static int pass_new(", "static float best_plain(float k) { return k / 1.0009765625f; }\n"
+                                                    "static int pass_new(")
+    p = tmp_path / "mut.c"
+    p.write_text(mutant)
+    exe = str(tmp_path / "mut")
+    subprocess.run(["gcc", "-O2", "-std=c11", "-ffp-contract=off", "-o", exe, str(p), "-lm"], check=True)
+    _, _, bad_old, bad_new, _, _ = _run(exe, 3_000_000, 1)
+    assert bad_old == 0 and bad_new > 0
