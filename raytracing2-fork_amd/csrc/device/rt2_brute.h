@@ -176,4 +176,50 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     flush_counters(L, p);
 }
 
+// SPLIT: the S waves of a workgroup trace the same 64 rays (same items, same
+// RNG streams, identical shading); wave w sweeps the w-th contiguous 1/S of the
+// triangle array, and the partial closest hits are combined through LDS in
+// wave order with strict < (a lower range wins a tie): the sequential scan's
+// (dst, index).  Per-ray latency falls by ~S at the same lane efficiency, for
+// launches with few items per lane (a 1/8 slab of config B on 8 GPUs).
+template <int S, int G, int FILT, int WPE>
+__global__ __launch_bounds__(64 * S) __attribute__((amdgpu_waves_per_eu(WPE))) void render_split(RenderParams p) {
+    __shared__ float part_best[S][64];
+    __shared__ int part_bi[S][64];
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // wave-uniform: scalar loads below
+    const int lane = (int)(threadIdx.x & 63);
+    const int per = ((p.n_tris + S - 1) / S + G - 1) / G * G;  // whole groups of G per wave
+    const int lo = min(w * per, p.n_tris), hi = min(lo + per, p.n_tris);
+    const float* tri = (const float*)p.tri + 12 * (size_t)lo;
+    Lane L;
+    lane_init(L);
+    for (;;) {
+        advance<S>(L, p);
+        if (!__any(L.st == ST_TRACE)) break;  // the same in every wave of the group
+        float best = 1e38f, bestK = 1e38f * 1.0009765625f;
+        int bi = -1;
+        if (L.st == ST_TRACE) sweep_masked<G, true, FILT>(L.o, L.d, nullptr, tri, hi - lo, lo, best, bi, bestK);
+        part_best[w][lane] = best;
+        part_bi[w][lane] = bi;
+        __syncthreads();
+        best = part_best[0][lane];
+        bi = part_bi[0][lane];
+#pragma unroll
+        for (int k = 1; k < S; k++) {
+            const float ob = part_best[k][lane];
+            if (ob < best) {
+                best = ob;
+                bi = part_bi[k][lane];
+            }
+        }
+        __syncthreads();
+        if (L.st == ST_TRACE) {
+            L.bounce += 1;
+            L.segs += 1;
+            shade<S>(L, p, best, bi);
+        }
+    }
+    flush_counters<S>(L, p);
+}
+
 }  // namespace

@@ -22,17 +22,35 @@ struct Lane {
     uint32_t t0;  // item start (s_memtime low bits), for the cost map
 };
 
+// S > 1: split mode (render_split) — the S waves of a workgroup hold the same
+// lanes (same items, same RNG streams, identical arithmetic) and each sweeps
+// 1/S of the triangles; wave 0 alone takes items and writes results.
+template <int S = 1>
+__device__ __forceinline__ bool split_writer() {
+    return S == 1 || threadIdx.x < 64;
+}
+template <int S = 1>
 __device__ __forceinline__ void end_path(Lane& L, const RenderParams& p);
 
-// Phase A: bring every lane to ST_TRACE or ST_DONE (wave-collective).
+// Phase A: bring every lane to ST_TRACE or ST_DONE (wave-collective; with
+// S > 1 workgroup-collective, every wave of the group on the same path).
+template <int S = 1>
 __device__ __forceinline__ void advance(Lane& L, const RenderParams& p) {
     for (;;) {
         const bool need = L.st == ST_NEED_ITEM;
         const unsigned long long m = __ballot(need);
         if (m) {
             unsigned long long base = 0;
-            if (lane_id() == 0) base = atomicAdd(p.item_counter, (unsigned long long)__popcll(m));
-            base = __shfl(base, 0);
+            if constexpr (S == 1) {
+                if (lane_id() == 0) base = atomicAdd(p.item_counter, (unsigned long long)__popcll(m));
+                base = __shfl(base, 0);
+            } else {
+                __shared__ unsigned long long split_base;
+                if (threadIdx.x == 0) split_base = atomicAdd(p.item_counter, (unsigned long long)__popcll(m));
+                __syncthreads();
+                base = split_base;
+                __syncthreads();
+            }
             if (need) {
                 unsigned long long it = base + lanes_below(m);
                 if (it < p.n_items) {
@@ -80,7 +98,7 @@ __device__ __forceinline__ void advance(Lane& L, const RenderParams& p) {
             L.incoming = mk(0.0f, 0.0f, 0.0f);
             L.bounce = 0;
             L.st = ST_TRACE;
-            if (p.maxBounce <= 0) end_path(L, p);  // trace() returns 0 without tracing
+            if (p.maxBounce <= 0) end_path<S>(L, p);  // trace() returns 0 without tracing
         }
         if (!__any(L.st != ST_TRACE && L.st != ST_DONE)) break;
     }
@@ -88,6 +106,7 @@ __device__ __forceinline__ void advance(Lane& L, const RenderParams& p) {
 
 // End of a path: colorCumulative += trace(...) (compute.glsl:692); next ray,
 // or end of the frame (compute.glsl:696-700 + the screenshot accumulation).
+template <int S>
 __device__ __forceinline__ void end_path(Lane& L, const RenderParams& p) {
     L.colorCum = add(L.colorCum, L.incoming);
     L.ray += 1;
@@ -97,25 +116,29 @@ __device__ __forceinline__ void end_path(Lane& L, const RenderParams& p) {
     }
     f3 c = divs(L.colorCum, (float)p.R);
     c = mk(srgb1(aces1(c.x)), srgb1(aces1(c.y)), srgb1(aces1(c.z)));
+    const bool writer = split_writer<S>();
     if (p.frame_split) {  // frame_accumulate adds the frames in order afterwards
-        p.frame_buf[(size_t)L.frame * p.n_pix + L.item] = make_float4(c.x, c.y, c.z, 0.0f);
-        if (p.cost_out) p.cost_out[L.item] = (uint32_t)__builtin_amdgcn_s_memtime() - L.t0;
+        if (writer) p.frame_buf[(size_t)L.frame * p.n_pix + L.item] = make_float4(c.x, c.y, c.z, 0.0f);
+        if (writer && p.cost_out) p.cost_out[L.item] = (uint32_t)__builtin_amdgcn_s_memtime() - L.t0;
         L.st = ST_NEED_ITEM;
         return;
     }
     // accumulate this frame in frame order: acc = acc + colour
-    const float4 a = p.accum[L.item];
-    p.accum[L.item] = make_float4(a.x + c.x, a.y + c.y, a.z + c.z, 0.0f);
-    if (p.accum8) {
-        // GL float -> unorm8, round to nearest (GL 4.3 §2.3.5.2)
-        const uint4 q = p.accum8[L.item];
-        p.accum8[L.item] = make_uint4(q.x + (uint32_t)(clampf(c.x, 0.0f, 1.0f) * 255.0f + 0.5f),
-                                      q.y + (uint32_t)(clampf(c.y, 0.0f, 1.0f) * 255.0f + 0.5f),
-                                      q.z + (uint32_t)(clampf(c.z, 0.0f, 1.0f) * 255.0f + 0.5f), 0u);
+    if (writer) {
+        const float4 a = p.accum[L.item];
+        p.accum[L.item] = make_float4(a.x + c.x, a.y + c.y, a.z + c.z, 0.0f);
+        if (p.accum8) {
+            // GL float -> unorm8, round to nearest (GL 4.3 §2.3.5.2)
+            const uint4 q = p.accum8[L.item];
+            p.accum8[L.item] = make_uint4(q.x + (uint32_t)(clampf(c.x, 0.0f, 1.0f) * 255.0f + 0.5f),
+                                          q.y + (uint32_t)(clampf(c.y, 0.0f, 1.0f) * 255.0f + 0.5f),
+                                          q.z + (uint32_t)(clampf(c.z, 0.0f, 1.0f) * 255.0f + 0.5f), 0u);
+        }
     }
     L.frame += 1;
     L.st = L.frame < p.frame_count ? ST_NEW_FRAME : ST_NEED_ITEM;
-    if (L.st == ST_NEED_ITEM && p.cost_out) p.cost_out[L.item] = (uint32_t)__builtin_amdgcn_s_memtime() - L.t0;
+    if (L.st == ST_NEED_ITEM && writer && p.cost_out)
+        p.cost_out[L.item] = (uint32_t)__builtin_amdgcn_s_memtime() - L.t0;
 }
 
 // texture(sampler2D, uv) with GL_LINEAR (no mipmaps) + GL_REPEAT, GL 4.3
@@ -168,6 +191,7 @@ __device__ __forceinline__ f3 texture_color(const RenderParams& p, int tex_index
 }
 
 // Phase C: scatter at the closest hit (compute.glsl:485-559).
+template <int S = 1>
 __device__ __forceinline__ void shade(Lane& L, const RenderParams& p, float best, int bi) {
     if (bi >= 0) {
         const int mi = p.tri_mtl[bi];
@@ -202,7 +226,7 @@ __device__ __forceinline__ void shade(Lane& L, const RenderParams& p, float best
         case RT2_LIGHT: {
             f3 emitted = muls(xyz4(m.emissionColor), m.emissionStrength);
             L.incoming = add(L.incoming, mul(emitted, L.rayColor));
-            end_path(L, p);
+            end_path<S>(L, p);
             return;
         }
         case RT2_CHECKER: {
@@ -227,7 +251,7 @@ __device__ __forceinline__ void shade(Lane& L, const RenderParams& p, float best
         }
         default:  // GLASS_HIGHLIGHT and unknown types: trace() returns magenta
             L.incoming = mk(1.0f, 0.0f, 1.0f);
-            end_path(L, p);
+            end_path<S>(L, p);
             return;
         }
         if (m.isEdgeHighlight && L.bounce > 1)
@@ -236,14 +260,14 @@ __device__ __forceinline__ void shade(Lane& L, const RenderParams& p, float best
             L.rayColor = mul(L.rayColor, atten);
         float pr = fmaxf(L.rayColor.x, fmaxf(L.rayColor.y, L.rayColor.z));
         if (rnd(L.seed) > pr) {
-            end_path(L, p);
+            end_path<S>(L, p);
             return;
         }
         L.rayColor = muls(L.rayColor, 1.0f / pr);
-        if (L.bounce >= p.maxBounce) end_path(L, p);
+        if (L.bounce >= p.maxBounce) end_path<S>(L, p);
     } else {
         if (p.envLight) L.incoming = add(L.incoming, mul(sky(L.d), L.rayColor));
-        end_path(L, p);
+        end_path<S>(L, p);
     }
 }
 
@@ -261,10 +285,11 @@ __device__ __forceinline__ void lane_init(Lane& L) {
     L.t0 = 0;
 }
 
+template <int S = 1>
 __device__ __forceinline__ void flush_counters(const Lane& L, const RenderParams& p) {
     unsigned long long s = L.segs;
     for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-    if (lane_id() == 0) atomicAdd(p.seg_counter, s);
+    if (lane_id() == 0 && split_writer<S>()) atomicAdd(p.seg_counter, s);
 }
 
 }  // namespace

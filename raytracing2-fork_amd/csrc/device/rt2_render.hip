@@ -395,7 +395,7 @@ namespace {
 constexpr int kTileTris = 1024;  // 48 KiB of LDS per tile
 
 // Kernel variants (rt2_scene_set_variant); 0 = auto = the default below.
-enum Kind : int { K_RESIDENT = 0, K_TILED = 1, K_SMEM = 2, K_BVH = 3, K_BVH2 = 4, K_BVH3 = 5 };
+enum Kind : int { K_RESIDENT = 0, K_TILED = 1, K_SMEM = 2, K_SPLIT = 3, K_BVH = 4, K_BVH2 = 5, K_BVH3 = 6 };
 struct Variant {
     int kind;
     int block;
@@ -410,6 +410,9 @@ hipError_t launch_t(const RenderParams& p, int blocks, size_t lds, hipStream_t s
         hipLaunchKernelGGL((render_tiled<BLOCK, MT, UNROLL>), dim3(blocks), dim3(BLOCK), lds, st, p);
     else if constexpr (KIND == K_SMEM)
         hipLaunchKernelGGL((render_smem<BLOCK, MT % 1000, MT / 1000, UNROLL>), dim3(blocks), dim3(BLOCK), 0, st, p);
+    else if constexpr (KIND == K_SPLIT)
+        hipLaunchKernelGGL((render_split<BLOCK / 64, MT % 1000, MT / 1000, UNROLL>), dim3(blocks), dim3(BLOCK), 0, st,
+                           p);
     else if constexpr (KIND == K_BVH)
         hipLaunchKernelGGL((render_bvh<BLOCK>), dim3(blocks), dim3(BLOCK), lds, st, p);
     else if constexpr (KIND == K_BVH2)
@@ -428,6 +431,9 @@ hipError_t occ_t(int* occ, size_t lds) {
     else if constexpr (KIND == K_SMEM)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_smem<BLOCK, MT % 1000, MT / 1000, UNROLL>,
                                                             BLOCK, 0);
+    else if constexpr (KIND == K_SPLIT)
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            occ, render_split<BLOCK / 64, MT % 1000, MT / 1000, UNROLL>, BLOCK, 0);
     else if constexpr (KIND == K_BVH)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_bvh<BLOCK>, BLOCK, lds);
     else if constexpr (KIND == K_BVH2)
@@ -511,6 +517,10 @@ const Variant kVariants[] = {
     RT2_VARIANT(K_SMEM, 256, 32508, 1, "smem/256/max3f8/coop32"),    // 67
     RT2_VARIANT(K_SMEM, 256, 32504, 1, "smem/256/max3f4/coop32"),    // 68
     RT2_VARIANT(K_SMEM, 256, 32508, 6, "smem/256/max3f8/coop32/w6"), // 69
+    RT2_VARIANT(K_SPLIT, 128, 8, 5, "split2/masked8/w5"),            // 70
+    RT2_VARIANT(K_SPLIT, 256, 8, 5, "split4/masked8/w5"),            // 71
+    RT2_VARIANT(K_SPLIT, 128, 1008, 5, "split2/max3f8/w5"),          // 72
+    RT2_VARIANT(K_SPLIT, 256, 1008, 5, "split4/max3f8/w5"),          // 73
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr size_t kResidentMaxBytes = 112 * 1024;
@@ -710,7 +720,8 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     HIPCHECK(V.occupancy(&occ, lds));
     occ = std::max(occ, 1);
     unsigned long long blocks = (unsigned long long)s->num_cus * occ;
-    blocks = std::min(blocks, (p.n_items + V.block - 1) / V.block);
+    const int rays_per_block = V.kind == K_SPLIT ? 64 : V.block;  // split: S waves per 64 rays
+    blocks = std::min(blocks, (p.n_items + rays_per_block - 1) / rays_per_block);
     blocks = std::max(blocks, 1ull);
     s->last_variant = vi;
     HIPCHECK(V.launch(p, (int)blocks, lds, st));
@@ -742,8 +753,8 @@ extern "C" int rt2_scene_stats(rt2_scene* s, rt2_stats* out, int reset) {
     out->segments = c[1];
     // brute force tests every triangle per segment; the BVH kernel counts its
     // leaf tests in c[2]
-    out->tests = s->last_kind == 3 ? c[2] : c[1] * (unsigned long long)s->n_tris;
-    out->node_visits = s->last_kind == 3 ? c[3] : 0;
+    out->tests = s->last_kind == K_BVH ? c[2] : c[1] * (unsigned long long)s->n_tris;
+    out->node_visits = s->last_kind == K_BVH ? c[3] : 0;
     if (reset) {
         s->samples = 0;
         HIPCHECK(hipMemset(s->d_counters, 0, sizeof(c)));

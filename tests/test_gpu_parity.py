@@ -258,7 +258,7 @@ def test_frame_split_identical(rt2mod, oraclemod, config_scene, torch_cuda, trav
 
 # brute-force kernel variants that change the schedule, not the arithmetic:
 # masked/ballot/min-filter sweeps, cooperative and team tail modes, occupancy hints
-BRUTE_VARIANTS = [0, 1, 2, 22, 24, 28, 31, 52, 59, 60, 64, 65, 66, 67, 68, 69]
+BRUTE_VARIANTS = [0, 1, 2, 22, 24, 28, 31, 52, 59, 60, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73]
 
 
 @pytest.mark.parametrize("variant", BRUTE_VARIANTS)
@@ -273,6 +273,32 @@ def test_brute_variants_bit_exact(rt2mod, oraclemod, config_scene, torch_cuda, v
     ref, _, segs = oracle_mean(oraclemod, sd, u, np.arange(H), 0, 2)
     assert_exact(img, ref, f"variant {variant}")
     assert st.segments == segs
+
+
+@pytest.mark.parametrize("variant", [71, 72])
+@pytest.mark.parametrize("split_frames", [False, True])
+def test_split_waves_outputs(rt2mod, oraclemod, config_scene, torch_cuda, variant, split_frames):
+    """Split mode (S waves per 64 rays, one writer wave): the float and 8-bit
+    accumulators, the per-frame planes and the counters see each pixel-frame
+    once — identical to the default kernel on a shard slab with 3 frames."""
+    sd, spec = config_scene("B")
+    W, H, R, F = 80, 45, 4, 3
+    u = rt2mod.offline_uniforms(W, H, spec.bounces, R, sd.num_triangles)
+    sh = rt2mod.shard(2, 1, 3)
+    out = {}
+    for v in (0, variant):
+        scene = rt2mod.Scene(sd, 0)
+        scene.set_variant(v)
+        scene.set_frame_split(split_frames)
+        out[v] = scene.render_host(u, 1, F, sh, rgb8=True)
+        st = scene.stats(reset=True)
+        out[v] += (st.segments, st.tests)
+    assert np.array_equal(out[0][0], out[variant][0])
+    assert np.array_equal(out[0][1], out[variant][1])
+    assert out[0][2:] == out[variant][2:]
+    rows = rt2mod.shard_row_ids(H, sh)
+    ref, _, _ = oracle_mean(oraclemod, sd, u, rows, 1, F)
+    assert_exact(out[variant][0], ref, f"split-wave variant {variant}")
 
 
 @pytest.mark.parametrize("variant", [64, 66])
