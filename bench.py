@@ -38,7 +38,7 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec
 FLOP_PER_TEST = 53
 FLOP_PER_VISIT = 24        # BVH interior node: 2 boxes x (6 sub + 6 div), compute.glsl:382-408
 BYTES_PER_TEST = 36        # a, b, c positions
-KERNEL_NAMES = {"brute": "render_smem (rt2_render.hip, variant smem/256/masked8/coop32)",
+KERNEL_NAMES = {"brute": "render_smem (rt2_render.hip, variant smem/256/max3f8/coop32/w6)",
                 "bvh": "render_bvh3 (rt2_render.hip, variant bvh3/256/t16/w5)"}
 
 

@@ -107,9 +107,11 @@ __global__ __launch_bounds__(BLOCK) void render_tiled(RenderParams p) {
 // COOP > 0: drain mode — once the item pool is exhausted (some lane is DONE)
 // and at most COOP lanes of the wave still trace, each live ray's closest hit
 // is computed by the whole wave (coop_closest), one ray at a time.
-template <int BLOCK, int G, int COOP, int WPE>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void render_smem(RenderParams p) {
+template <int BLOCK, int G, int COOP>
+__device__ __forceinline__ void smem_body(const RenderParams& p) {
     cfloat* tri = (cfloat*)p.tri;
+    constexpr bool kStats = G >= 700 && G < 900;  // diagnostic builds: filter survivor counters
+    FiltStats fs;
     Lane L;
     lane_init(L);
     for (;;) {
@@ -157,7 +159,25 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             float best = 1e38f, bestK = 1e38f * 1.0009765625f;
             int bi = -1;
             const f3 o = L.o, d = L.d;
-            if constexpr (G >= 500)
+            if constexpr (G >= 800) {
+                sweep_masked<G - 800, true, 1, true>(o, d, nullptr, (const float*)p.tri, p.n_tris, 0, best, bi, bestK,
+                                                    &fs);
+            } else if constexpr (G >= 700) {
+                if (p.plk && __ballot(!plk_lane_ok(o, d)) == 0)
+                    sweep_plk<G - 700, true>(o, d, (const float*)p.plk, (const float*)p.tri, p.n_tris, p.plk_A, best,
+                                             bi, bestK, &fs);
+                else
+                    sweep_masked<8, true, 1, true>(o, d, nullptr, (const float*)p.tri, p.n_tris, 0, best, bi, bestK,
+                                                   &fs);
+            } else if constexpr (G >= 600) {
+                // per-ray precomputed filter when the scene and every tracing
+                // lane of the wave are inside its validated range
+                if (p.plk && __ballot(!plk_lane_ok(o, d)) == 0)
+                    sweep_plk<G - 600>(o, d, (const float*)p.plk, (const float*)p.tri, p.n_tris, p.plk_A, best, bi,
+                                       bestK);
+                else
+                    sweep_masked<8, true, 1>(o, d, nullptr, (const float*)p.tri, p.n_tris, 0, best, bi, bestK);
+            } else if constexpr (G >= 500)
                 sweep_masked<G - 500, true, 1>(o, d, nullptr, (const float*)p.tri, p.n_tris, 0, best, bi, bestK);
             else if constexpr (G >= 400)
                 sweep_minfilter<G - 400>(o, d, (const float*)p.tri, p.n_tris, best, bi, bestK);
@@ -173,9 +193,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             shade(L, p, best, bi);
         }
     }
+    if constexpr (kStats) fs.flush(p.seg_counter + 20);
     flush_counters(L, p);
 }
 
+template <int BLOCK, int G, int COOP, int WPE>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void render_smem(RenderParams p) {
+    smem_body<BLOCK, G, COOP>(p);
+}
 // SPLIT: the S waves of a workgroup trace the same 64 rays (same items, same
 // RNG streams, identical shading); wave w sweeps the w-th contiguous 1/S of the
 // triangle array, and the partial closest hits are combined through LDS in

@@ -415,7 +415,7 @@ __device__ __forceinline__ void bvh_interior3(TravState3& T, int* st, int e, con
     const float4* rp = recs + 4 * e;
     const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
     const float4 r3 = rp[3];
-    float dA, dB;
+    float dA = 1e38f, dB = 1e38f;  // set by the filter (DIV 2) or the exact forms below
     bool exact = true;
     if (fast && DIV == 2) {
         float aMin, aMax, bMin, bMax;

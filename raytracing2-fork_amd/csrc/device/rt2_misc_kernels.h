@@ -219,6 +219,64 @@ __global__ void prep_triangles(const rt2_triangle* tris, int n, float4* out, int
     mtl[i] = t.materialIndex;
 }
 
+// sweep_plk records (rt2_sweep.h) from the pre-transformed triangles, in
+// binary64: p0 = a×e0, p1 = a×e1 and a·n are rounded once to binary32 after
+// the exact power-of-two scale s (s·max(|e0|,|e1|,|n|)∞ in [1,2)).  The
+// filter's error bound holds for |a_i| <= 2^20, every component of e0/e1/n 0
+// or in [2^-100, 2^20], and max(|e0|,|e1|,|n|)∞ >= 2^-30; a triangle outside
+// that range (or non-finite, or degenerate) gets the all-zero record, which
+// always passes (the exact test decides), and is counted in flags[0].
+// flags[1] = max |a_i| over the in-range triangles (float bits: an atomic max
+// over non-negative floats).
+__global__ void prep_plk(const float4* tri, int n, float4* out, uint32_t* flags) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float4 t0 = tri[3 * i], t1 = tri[3 * i + 1], t2 = tri[3 * i + 2];
+    const float a[3] = {t0.x, t0.y, t0.z}, e0[3] = {t0.w, t1.x, t1.y}, e1[3] = {t1.z, t1.w, t2.x},
+                nn[3] = {t2.y, t2.z, t2.w};
+    bool ok = true;
+    float A = 0.0f, M = 0.0f;
+    for (int k = 0; k < 3; k++) {
+        ok = ok && fabsf(a[k]) <= 0x1p20f;  // false for NaN
+        A = fmaxf(A, fabsf(a[k]));
+        for (float x : {e0[k], e1[k], nn[k]}) {
+            const float ax = fabsf(x);
+            ok = ok && (x == 0.0f || (ax >= 0x1p-100f && ax <= 0x1p20f));
+            M = fmaxf(M, ax);
+        }
+    }
+    ok = ok && M >= 0x1p-30f;
+    float r[16];
+    for (int k = 0; k < 16; k++) r[k] = 0.0f;
+    if (ok) {
+        int ex;
+        (void)frexpf(M, &ex);  // M = f * 2^ex, f in [0.5, 1)
+        const double s = ldexp(1.0, 1 - ex);
+        auto D = [](float x) { return (double)x; };
+        const double p0[3] = {D(a[1]) * e0[2] - D(a[2]) * e0[1], D(a[2]) * e0[0] - D(a[0]) * e0[2],
+                              D(a[0]) * e0[1] - D(a[1]) * e0[0]};
+        const double p1[3] = {D(a[1]) * e1[2] - D(a[2]) * e1[1], D(a[2]) * e1[0] - D(a[0]) * e1[2],
+                              D(a[0]) * e1[1] - D(a[1]) * e1[0]};
+        const double an = D(a[0]) * nn[0] + D(a[1]) * nn[1] + D(a[2]) * nn[2];
+        for (int k = 0; k < 3; k++) {
+            r[k] = (float)(nn[k] * s);
+            r[4 + k] = (float)(e0[k] * s);
+            r[10 + k] = (float)(e1[k] * s);
+        }
+        r[3] = (float)(-an * s);
+        r[7] = (float)(-p0[0] * s);
+        r[8] = (float)(-p0[1] * s);
+        r[9] = (float)(-p0[2] * s);
+        r[13] = (float)(-p1[0] * s);
+        r[14] = (float)(-p1[1] * s);
+        r[15] = (float)(-p1[2] * s);
+        atomicMax(&flags[1], __float_as_uint(A));
+    } else {
+        atomicAdd(&flags[0], 1u);
+    }
+    for (int k = 0; k < 4; k++) out[4 * i + k] = make_float4(r[4 * k], r[4 * k + 1], r[4 * k + 2], r[4 * k + 3]);
+}
+
 __global__ void resolve_kernel(const float4* acc, long long n, float inv_frames_dummy, float frames, float4* out) {
     long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;

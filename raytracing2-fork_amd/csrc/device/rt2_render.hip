@@ -64,6 +64,10 @@ struct rt2_scene {
     rt2_material* d_mats = nullptr;
     rt2_node* d_nodes = nullptr;
     float4* d_recs = nullptr;                   // BVH v2 child-pair records
+    float4* d_plk = nullptr;                    // sweep_plk filter records (4 float4 per triangle)
+    int plk_ok = 0;                             // sweep_plk usable: <= 1/64 of the triangles outside its range
+    int plk_outside = 0;                        // triangles with an always-pass record
+    float plk_A = 0.0f;                         // max |a_i| over the triangles
     float4* d_fb = nullptr;                     // frame_split scratch (per-frame colours)
     uchar4* d_texels = nullptr;                 // textures, RGBA8
     int4* d_tex_desc = nullptr;
@@ -346,6 +350,18 @@ extern "C" int rt2_scene_create(const rt2_triangle* tris, int32_t n_tris, const 
         hipLaunchKernelGGL(prep_triangles, dim3((n_tris + 255) / 256), dim3(256), 0, 0, s->d_raw, n_tris, s->d_tri,
                            s->d_mtl);
         HIPCHECK(hipGetLastError());
+        HIPCHECK(hipMalloc(&s->d_plk, nt * 4 * sizeof(float4)));
+        uint32_t* d_flags = nullptr;
+        HIPCHECK(hipMalloc(&d_flags, 2 * sizeof(uint32_t)));
+        HIPCHECK(hipMemset(d_flags, 0, 2 * sizeof(uint32_t)));
+        hipLaunchKernelGGL(prep_plk, dim3((n_tris + 255) / 256), dim3(256), 0, 0, s->d_tri, n_tris, s->d_plk, d_flags);
+        HIPCHECK(hipGetLastError());
+        uint32_t flags[2];
+        HIPCHECK(hipMemcpy(flags, d_flags, sizeof(flags), hipMemcpyDeviceToHost));
+        HIPCHECK(hipFree(d_flags));
+        s->plk_outside = (int)flags[0];
+        s->plk_ok = (unsigned long long)flags[0] * 64 <= (unsigned long long)n_tris;  // <= 1/64 always-pass records
+        std::memcpy(&s->plk_A, &flags[1], sizeof(float));
     }
     HIPCHECK(hipDeviceSynchronize());
     *out = s;
@@ -361,6 +377,7 @@ extern "C" void rt2_scene_destroy(rt2_scene* s) {
     (void)hipFree(s->d_mats);
     (void)hipFree(s->d_nodes);
     (void)hipFree(s->d_recs);
+    (void)hipFree(s->d_plk);
     (void)hipFree(s->d_fb);
     (void)hipFree(s->d_cost);
     (void)hipFree(s->d_order);
@@ -447,7 +464,7 @@ hipError_t occ_t(int* occ, size_t lds) {
 #define RT2_VARIANT(T, B, M, U, NAME) Variant{T, B, launch_t<T, B, M, U>, occ_t<T, B, M, U>, NAME}
 
 const Variant kVariants[] = {
-    RT2_VARIANT(K_SMEM, 256, 32108, 1, "smem/256/masked8/coop32"),   // 0: default (<= kSmemMaxTris)
+    RT2_VARIANT(K_SMEM, 256, 32508, 6, "smem/256/max3f8/coop32/w6"), // 0: default (<= kSmemMaxTris)
     RT2_VARIANT(K_RESIDENT, 256, 0, 4, "resident/256/plain/u4"),     // 1: round-1 v1 kernel
     RT2_VARIANT(K_TILED, 512, 4, 1, "tiled/512/grouped4"),           // 2: default (large scenes)
     RT2_VARIANT(K_RESIDENT, 256, 1, 4, "resident/256/filtered/u4"),  // 3
@@ -521,11 +538,24 @@ const Variant kVariants[] = {
     RT2_VARIANT(K_SPLIT, 256, 8, 5, "split4/masked8/w5"),            // 71
     RT2_VARIANT(K_SPLIT, 128, 1008, 5, "split2/max3f8/w5"),          // 72
     RT2_VARIANT(K_SPLIT, 256, 1008, 5, "split4/max3f8/w5"),          // 73
+    RT2_VARIANT(K_SMEM, 256, 32604, 1, "smem/256/plk4/coop32"),      // 74
+    RT2_VARIANT(K_SMEM, 256, 32606, 1, "smem/256/plk6/coop32"),      // 75
+    RT2_VARIANT(K_SMEM, 256, 32608, 1, "smem/256/plk8/coop32"),      // 76
+    RT2_VARIANT(K_SMEM, 256, 32604, 6, "smem/256/plk4/coop32/w6"),   // 77
+    RT2_VARIANT(K_SMEM, 256, 32606, 6, "smem/256/plk6/coop32/w6"),   // 78
+    RT2_VARIANT(K_SMEM, 256, 32608, 6, "smem/256/plk8/coop32/w6"),   // 79
+    RT2_VARIANT(K_SMEM, 256, 32602, 1, "smem/256/plk2/coop32"),      // 80
+    RT2_VARIANT(K_SMEM, 256, 32704, 1, "smem/256/plk4/coop32/STATS"), // 81: diagnostic counters
+    RT2_VARIANT(K_SMEM, 256, 32808, 1, "smem/256/max3f8/coop32/STATS"), // 82: diagnostic counters
+    RT2_VARIANT(K_SPLIT, 512, 8, 4, "split8/masked8/w4"),            // 83
+    RT2_VARIANT(K_SPLIT, 512, 1008, 4, "split8/max3f8/w4"),          // 84
+    RT2_VARIANT(K_SPLIT, 256, 1008, 6, "split4/max3f8/w6"),          // 85
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr size_t kResidentMaxBytes = 112 * 1024;
 constexpr int kSmemMaxTris = 16384;
 constexpr int kDefaultBvhVariant = 53;
+constexpr int kSmallSlabVariant = 85;  // split4/max3f8/w6: brute force on slabs with fewer items than lanes
 }  // namespace
 
 extern "C" const char* rt2_variant_name(int v) { return v >= 0 && v < kNumVariants ? kVariants[v].name : nullptr; }
@@ -568,6 +598,8 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     RenderParams p;
     std::memset(&p, 0, sizeof(p));
     p.tri = s->d_tri;
+    p.plk = s->plk_ok ? s->d_plk : nullptr;
+    p.plk_A = s->plk_A;
     p.tri_mtl = s->d_mtl;
     p.raw = s->d_raw;
     p.texels = s->d_texels;
@@ -700,8 +732,20 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
         if (vi <= 0 || vi >= kNumVariants || kVariants[vi].kind < K_BVH)
             vi = kDefaultBvhVariant;
     } else {
-        if (vi <= 0 || vi >= kNumVariants || kVariants[vi].kind >= K_BVH)
+        if (vi <= 0 || vi >= kNumVariants || kVariants[vi].kind >= K_BVH) {
             vi = s->n_tris <= kSmemMaxTris ? 0 : 2;
+            if (vi == 0) {
+                // fewer items than resident lanes (a 1/8 slab of config B: 259k
+                // pixels, 393k lanes): every lane owns at most one long item and
+                // the launch is its tail; the split-wave kernel traces each 64
+                // rays with S waves (1/S of the triangles each)
+                int occ0 = 0;
+                HIPCHECK(kVariants[0].occupancy(&occ0, 0));
+                const unsigned long long lanes =
+                    (unsigned long long)s->num_cus * (unsigned long long)std::max(occ0, 1) * kVariants[0].block;
+                if (p.n_items < lanes) vi = kSmallSlabVariant;
+            }
+        }
         if (kVariants[vi].kind == K_RESIDENT && !fits) vi = 2;  // a resident variant cannot hold this scene
     }
     const Variant& V = kVariants[vi];
@@ -852,6 +896,16 @@ extern "C" int rt2_scene_diag_ex(rt2_scene* s, unsigned long long* out, int n) {
     if (!s || !out || n < 0) return -1;
     std::memcpy(out, s->diag, sizeof(unsigned long long) * (size_t)std::min(n, kCounters));
     return std::min(n, kCounters);
+}
+
+// Not in rt2.h (diagnostics): whether the scene's triangles admit sweep_plk,
+// its A (max |a_i|) and how many triangles carry an always-pass record.
+extern "C" int rt2_scene_plk_info(rt2_scene* s, int* ok, float* A, int* n_outside) {
+    if (!s) return -1;
+    if (ok) *ok = s->plk_ok;
+    if (A) *A = s->plk_A;
+    if (n_outside) *n_outside = s->plk_outside;
+    return 0;
 }
 
 extern "C" int rt2_scene_diag(rt2_scene* s, unsigned long long* out8, int* last_variant) {

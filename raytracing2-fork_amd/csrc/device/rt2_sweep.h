@@ -41,6 +41,8 @@ struct RenderParams {
     const int4* tex_desc;        // per texture {width, height, offset lo, offset hi}
     int n_tex;                   // textures uploaded
     int num_textures;            // uniforms.numTextures
+    const float4* plk;           // nullable: per-ray-precomputed filter records (sweep_plk), 4 float4 each
+    float plk_A;                 // max |a_i| over the scene's triangles (sweep_plk error bound)
 };
 
 enum : int { ST_NEED_ITEM = 0, ST_NEW_FRAME = 1, ST_NEW_RAY = 2, ST_TRACE = 3, ST_DONE = 4 };
@@ -57,6 +59,33 @@ __device__ __forceinline__ int shard_row(int local_row, int tile_rows, int rank,
     int t = local_row / tile_rows;
     return (t * nranks + rank) * tile_rows + local_row % tile_rows;
 }
+
+// Survivor counters of the brute sweeps (diagnostic variants only): tests a
+// wave evaluated, tests where some lane passed the filter, lane survivors.
+struct FiltStats {
+    unsigned long long tests = 0, wave_any = 0, lanes = 0;
+    __device__ __forceinline__ void add(bool f) {
+        const unsigned long long act = __ballot(true), m = __ballot(f);
+        if (lane_id() == (uint32_t)__builtin_ctzll(act)) {  // once per wave-test
+            tests += 1;
+            wave_any += m != 0;
+        }
+        lanes += f;
+    }
+    __device__ __forceinline__ void flush(unsigned long long* c) {
+        unsigned long long t = tests, w = wave_any, l = lanes;
+        for (int off = 32; off > 0; off >>= 1) {
+            t += __shfl_xor(t, off);
+            w += __shfl_xor(w, off);
+            l += __shfl_xor(l, off);
+        }
+        if (lane_id() == 0) {
+            atomicAdd(c + 0, t);
+            atomicAdd(c + 1, w);
+            atomicAdd(c + 2, l);
+        }
+    }
+};
 
 // One Möller–Trumbore test (compute.glsl:302-340) against a pre-transformed
 // triangle; updates the running closest hit (compute.glsl:432-434).
@@ -291,9 +320,10 @@ __device__ __forceinline__ void mt_exact(const MtQ& q, int idx, float& best, int
 // per-lane bit packing); phase 2 runs mt_exact under each mask in index order
 // (skipped by a scalar branch when the mask is empty).  SMEM selects the
 // scalar-load path for the triangle records instead of LDS.
-template <int G, bool SMEM, int FILT = 0>
+template <int G, bool SMEM, int FILT = 0, bool STATS = false>
 __device__ __forceinline__ void sweep_masked(const f3& o, const f3& d, const float4* lds, const float* gtri,
-                                             int count, int base, float& best, int& bi, float& bestK) {
+                                             int count, int base, float& best, int& bi, float& bestK,
+                                             FiltStats* fs = nullptr) {
     int i = 0;
     for (; i + G <= count; i += G) {
         MtQ q[G];
@@ -314,6 +344,7 @@ __device__ __forceinline__ void sweep_masked(const f3& o, const f3& d, const flo
             }
             q[k] = mt_quantities(o, d, t0, t1, t2);
             f[k] = mt_pass_f<FILT>(q[k], bestK);
+            if constexpr (STATS) fs->add(f[k]);
         }
 #pragma unroll
         for (int k = 0; k < G; k++)
@@ -335,6 +366,79 @@ __device__ __forceinline__ void sweep_masked(const f3& o, const f3& d, const flo
         const MtQ q = mt_quantities(o, d, t0, t1, t2);
         if (mt_pass_f<FILT>(q, bestK)) mt_exact(q, base + i, best, bi, bestK);
     }
+}
+
+// Per-ray precomputed filter ("plk" records).  The reference intermediates
+// are U = e1·(d×(o−a)), V = e0·(d×(o−a)), tnum = (o−a)·n.  By the triple
+// product identity they equal
+//     U = e1·m − d·p1,  V = e0·m − d·p0,  tnum = o·n − a·n,
+// with m = d×o once per segment and p0 = a×e0, p1 = a×e1, a·n once per
+// triangle (host-side in binary64).  That is 18 VALU for the four
+// quantities instead of 21, and the filter needs no per-test origin shift.
+// They are approximations U', V', tnum' of the reference's rounded values;
+// the filter compares against a threshold T that covers the error of both
+// ("The per-ray filter"):
+//   |U' − s·U_ref|, |V' − s·V_ref|, |tnum' − s·tnum_ref| <= 2^-16 (|o|∞ + A)
+//   T = 2^-13 (|o|∞ + A) + 2^-40                  (A = scene max |a|∞)
+// where s = 2^k is the triangle's record scale (s·max(|e0|,|e1|,|n|) in
+// [1,2)), so one threshold per segment serves every triangle.  The record
+// is valid only in the range the bound was derived for: the host checks it
+// per triangle (prep_plk: outside it a triangle's record always passes), the
+// kernel per segment (|o|∞ <= 2^20, |d|∞ <= 1.0001 — every direction the path
+// makes is unit length to a few ulps; otherwise the wave takes sweep_masked).  dn = d·n_s = −det_s;
+// bkf = bestK while it is <= 2^60, +inf before (or without) a near hit.
+// Pass iff max(U', −V', RN(V'−U') + c·dn, −tnum', tnum' + bkf·dn) <= T.
+// Survivors run the reference arithmetic (mt_quantities + mt_exact) on the
+// triangle's own record: the closest hit is bit-identical by construction.
+// Record (4 float4): {n_s, −a·n_s} {e0_s, −p0_s.x} {−p0_s.yz, e1_s.xy} {e1_s.z, −p1_s}.
+__device__ __forceinline__ bool plk_pass(const f3& o, const f3& d, const f3& m, float T, float bkf, cfloat* r) {
+    const float dn = __builtin_fmaf(d.z, r[2], __builtin_fmaf(d.y, r[1], d.x * r[0]));
+    const float tn = __builtin_fmaf(o.z, r[2], __builtin_fmaf(o.y, r[1], __builtin_fmaf(o.x, r[0], r[3])));
+    float V = __builtin_fmaf(r[6], m.z, __builtin_fmaf(r[5], m.y, r[4] * m.x));
+    V = __builtin_fmaf(d.z, r[9], __builtin_fmaf(d.y, r[8], __builtin_fmaf(d.x, r[7], V)));
+    float U = __builtin_fmaf(r[12], m.z, __builtin_fmaf(r[11], m.y, r[10] * m.x));
+    U = __builtin_fmaf(d.z, r[15], __builtin_fmaf(d.y, r[14], __builtin_fmaf(d.x, r[13], U)));
+    const float X = __builtin_fmaf(dn, 1.0009765625f, V - U);
+    const float Y = __builtin_fmaf(dn, bkf, tn);
+    return fmaxf(fmaxf(fmaxf(fmaxf(U, -V), X), -tn), Y) <= T;  // two v_max3_f32
+}
+template <int G, bool STATS = false>
+__device__ __forceinline__ void sweep_plk(const f3& o, const f3& d, const float* plk, const float* gtri, int count,
+                                          float A, float& best, int& bi, float& bestK, FiltStats* fs = nullptr) {
+    const f3 m = cross(d, o);
+    const float O = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+    const float T = __builtin_fmaf(0x1p-13f, O + A, 0x1p-40f);
+    float bkf = bestK <= 0x1p60f ? bestK : __builtin_inff();
+    int i = 0;
+    for (; i + G <= count; i += G) {
+        bool f[G];
+#pragma unroll
+        for (int k = 0; k < G; k++) {
+            f[k] = plk_pass(o, d, m, T, bkf, (cfloat*)plk + 16 * (i + k));
+            if constexpr (STATS) fs->add(f[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < G; k++) {
+            if (f[k]) {
+                cfloat* t = (cfloat*)gtri + 12 * (i + k);
+                mt_exact(mt_quantities(o, d, ldc4(t), ldc4(t + 4), ldc4(t + 8)), i + k, best, bi, bestK);
+                bkf = bestK <= 0x1p60f ? bestK : __builtin_inff();
+            }
+        }
+    }
+    for (; i < count; i++) {
+        if (plk_pass(o, d, m, T, bkf, (cfloat*)plk + 16 * i)) {
+            cfloat* t = (cfloat*)gtri + 12 * i;
+            mt_exact(mt_quantities(o, d, ldc4(t), ldc4(t + 4), ldc4(t + 8)), i, best, bi, bestK);
+            bkf = bestK <= 0x1p60f ? bestK : __builtin_inff();
+        }
+    }
+}
+// The segment's rays are inside the range sweep_plk's bound covers.
+__device__ __forceinline__ bool plk_lane_ok(const f3& o, const f3& d) {
+    const float O = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+    const float D = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
+    return O <= 0x1p20f && D <= 1.0001f;  // false for NaN and inf
 }
 
 // Ballot sweep: phase 1 computes G filters and turns them into wave masks

@@ -253,6 +253,7 @@ def lib() -> C.CDLL:
         "rt2_device_div_check": (C.c_int, [U32, C.c_ulonglong, C.c_int, C.POINTER(C.c_ulonglong), C.POINTER(U32)]),
         "rt2_variant_name": (C.c_char_p, [C.c_int]),
         "rt2_scene_diag": (C.c_int, [P, C.POINTER(C.c_ulonglong), C.POINTER(C.c_int)]),
+        "rt2_scene_plk_info": (C.c_int, [P, C.POINTER(C.c_int), C.POINTER(C.c_float), C.POINTER(C.c_int)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

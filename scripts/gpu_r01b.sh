@@ -1,0 +1,15 @@
+#!/bin/bash
+# Re-entry session GPU check: tests, smoke, bench, rocprof, then A/B of the
+# newest brute variants (max3 filter, split-wave) on config B and its 1/N slabs.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+{ grep -m1 "model name" /proc/cpuinfo; nproc; } > gpurun_out/host.txt 2>&1
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { echo "gpu tests failed"; exit 1; }
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; exit 1; }
+timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 || { echo "bench failed"; exit 1; }
+timeout -k 10 150 python scripts/ab_variants.py --variants 0,52,67,68,69 --rounds 3 > gpurun_out/ab_B.json 2>&1 || { echo "ab failed"; exit 1; }
+timeout -k 10 150 python scripts/shard_probe.py --variants 0,70,71,72,73 > gpurun_out/shard_B.log 2>&1 || { echo "shard probe failed"; exit 1; }
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --no-alt > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1 || { echo "rocprof failed"; exit 1; }
+echo "all ok"

@@ -8,9 +8,13 @@
  * with -ffp-contract=off), over random and adversarial rays: rays through
  * triangle edges and vertices nudged by a few ulps, grazing rays around the
  * det = 1e-10 cut, `best` at and around the hit distance, coordinates over
- * six decades.
+ * six decades.  The per-ray precomputed filter (sweep_plk, plk_pass) is
+ * checked the same way on its own record (built as prep_plk does, binary64
+ * then one rounding) with extra draws of small triangles far from the origin
+ * (the cancellation case of o·n − a·n).
  *
- *   filter_check <pairs> <seed>   ->  "pairs accepts violations_old violations_new pass_old pass_new"
+ *   filter_check <pairs> <seed>
+ *     -> "pairs accepts violations_old violations_new pass_old pass_new violations_plk pass_plk"
  */
 #include <math.h>
 #include <stdint.h>
@@ -77,15 +81,68 @@ static int pass_new(Q q, float bestK) {
     return fmaxf(fmaxf(fmaxf(q.U, -q.V), X), fmaxf(-q.tnum, Y)) <= B;
 }
 
+/* prep_plk (rt2_misc_kernels.h): record of one triangle; returns 0 when the
+ * triangle is outside the validated range (the scene keeps the old filter). */
+static int plk_record(f3 a, f3 e0, f3 e1, f3 n, float r[16], float* Aout) {
+    const float av[3] = {a.x, a.y, a.z}, e0v[3] = {e0.x, e0.y, e0.z}, e1v[3] = {e1.x, e1.y, e1.z},
+                nv[3] = {n.x, n.y, n.z};
+    float A = 0.0f, M = 0.0f;
+    int ok = 1;
+    for (int k = 0; k < 3; k++) {
+        ok = ok && fabsf(av[k]) <= 0x1p20f;
+        A = fmaxf(A, fabsf(av[k]));
+        const float xs[3] = {e0v[k], e1v[k], nv[k]};
+        for (int j = 0; j < 3; j++) {
+            const float ax = fabsf(xs[j]);
+            ok = ok && (xs[j] == 0.0f || (ax >= 0x1p-100f && ax <= 0x1p20f));
+            M = fmaxf(M, ax);
+        }
+    }
+    for (int k = 0; k < 16; k++) r[k] = 0.0f;  /* all-zero record: always passes */
+    *Aout = A;
+    if (!ok || !(M >= 0x1p-30f)) return 0;
+    int ex;
+    (void)frexpf(M, &ex);
+    const double s = ldexp(1.0, 1 - ex);
+    const double p0[3] = {(double)a.y * e0.z - (double)a.z * e0.y, (double)a.z * e0.x - (double)a.x * e0.z,
+                          (double)a.x * e0.y - (double)a.y * e0.x};
+    const double p1[3] = {(double)a.y * e1.z - (double)a.z * e1.y, (double)a.z * e1.x - (double)a.x * e1.z,
+                          (double)a.x * e1.y - (double)a.y * e1.x};
+    const double an = (double)a.x * n.x + (double)a.y * n.y + (double)a.z * n.z;
+    r[0] = (float)(n.x * s); r[1] = (float)(n.y * s); r[2] = (float)(n.z * s); r[3] = (float)(-an * s);
+    r[4] = (float)(e0.x * s); r[5] = (float)(e0.y * s); r[6] = (float)(e0.z * s); r[7] = (float)(-p0[0] * s);
+    r[8] = (float)(-p0[1] * s); r[9] = (float)(-p0[2] * s); r[10] = (float)(e1.x * s); r[11] = (float)(e1.y * s);
+    r[12] = (float)(e1.z * s); r[13] = (float)(-p1[0] * s); r[14] = (float)(-p1[1] * s); r[15] = (float)(-p1[2] * s);
+    return 1;
+}
+/* sweep_plk's segment constants and plk_pass */
+static int pass_plk(f3 o, f3 d, const float* r, float A, float bestK) {
+    const f3 m = cross(d, o);
+    const float O = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+    const float T = fmaf(0x1p-13f, O + A, 0x1p-40f);
+    const float bkf = bestK <= 0x1p60f ? bestK : INFINITY;
+    const float dn = fmaf(d.z, r[2], fmaf(d.y, r[1], d.x * r[0]));
+    const float tn = fmaf(o.z, r[2], fmaf(o.y, r[1], fmaf(o.x, r[0], r[3])));
+    float V = fmaf(r[6], m.z, fmaf(r[5], m.y, r[4] * m.x));
+    V = fmaf(d.z, r[9], fmaf(d.y, r[8], fmaf(d.x, r[7], V)));
+    float U = fmaf(r[12], m.z, fmaf(r[11], m.y, r[10] * m.x));
+    U = fmaf(d.z, r[15], fmaf(d.y, r[14], fmaf(d.x, r[13], U)));
+    const float X = fmaf(dn, 1.0009765625f, V - U);
+    const float Y = fmaf(dn, bkf, tn);
+    return fmaxf(fmaxf(fmaxf(fmaxf(U, -V), X), -tn), Y) <= T;
+}
+
 int main(int argc, char** argv) {
     const long long n = argc > 1 ? atoll(argv[1]) : 1000000;
     s_rng = argc > 2 ? strtoull(argv[2], 0, 10) * 0x9E3779B97F4A7C15ull + 1 : 88172645463325252ull;
-    long long accepts = 0, bad_old = 0, bad_new = 0, p_old = 0, p_new = 0;
+    long long accepts = 0, bad_old = 0, bad_new = 0, p_old = 0, p_new = 0, bad_plk = 0, p_plk = 0, p_plk_near = 0, p_old_near = 0;
     for (long long it = 0; it < n; it++) {
         const int kind = (int)(next64() % 6);
+        const int far = (next64() % 4) == 0;  /* small triangle far from the origin */
         const float scale = powf(10.0f, 4.0f * uni() - 2.0f);  /* 1e-2 .. 1e2 */
         const float tsz = scale * powf(10.0f, -3.0f * uni());
-        const f3 c0 = mk(scale * sym(), scale * sym(), scale * sym());
+        const float off = far ? powf(10.0f, 5.0f * uni()) * scale : 0.0f;
+        const f3 c0 = mk(off * sym() + scale * sym(), off * sym() + scale * sym(), off * sym() + scale * sym());
         const f3 a = c0;
         const f3 b = mk(c0.x + tsz * sym(), c0.y + tsz * sym(), c0.z + tsz * sym());
         const f3 c = mk(c0.x + tsz * sym(), c0.y + tsz * sym(), c0.z + tsz * sym());
@@ -99,6 +156,7 @@ int main(int argc, char** argv) {
         if (kind == 4) { wu = (float)(next64() & 1); wv = wu > 0.0f ? 0.0f : (float)(next64() & 1); }
         const f3 p = mk(a.x + wu * e0.x + wv * e1.x, a.y + wu * e0.y + wv * e1.y, a.z + wu * e0.z + wv * e1.z);
         f3 o = mk(c0.x + 2.0f * scale * sym(), c0.y + 2.0f * scale * sym(), c0.z + 2.0f * scale * sym());
+        if (far && (next64() & 1)) o = mk(2.0f * scale * sym(), 2.0f * scale * sym(), 2.0f * scale * sym());
         f3 d;
         if (kind == 5) {
             /* grazing: direction (nearly) in the triangle's plane */
@@ -125,12 +183,23 @@ int main(int argc, char** argv) {
         const float bestK = best * 1.0009765625f;
         const int ex = exact_updates(q, best);
         const int fo = pass_old(q, bestK), fn = pass_new(q, bestK);
+        float rec[16], A;
+        /* an out-of-range triangle keeps its all-zero record (always passes);
+         * the scene's A is at least this triangle's |a| */
+        (void)plk_record(a, e0, e1, nrm, rec, &A);
+        if (fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)) <= 0x1p20f) {
+            const int fp = pass_plk(o, d, rec, A, bestK);
+            p_plk += fp;
+            if (ex && !fp) bad_plk++;
+            if (!far) p_plk_near += fp, p_old_near += fo;
+        }
         accepts += ex;
         p_old += fo;
         p_new += fn;
         if (ex && !fo) bad_old++;
         if (ex && !fn) bad_new++;
     }
-    printf("%lld %lld %lld %lld %lld %lld\n", n, accepts, bad_old, bad_new, p_old, p_new);
+    printf("%lld %lld %lld %lld %lld %lld %lld %lld\n", n, accepts, bad_old, bad_new, p_old, p_new, bad_plk, p_plk);
+    fprintf(stderr, "near-origin draws: pass_old %lld pass_plk %lld\n", p_old_near, p_plk_near);
     return 0;
 }

@@ -1,7 +1,7 @@
 """The brute-force kernel's division-free filters never reject a pair the
 reference's Möller–Trumbore test accepts (CPU restatement of rt2_sweep.h
-mt_pass / mt_pass3 in binary32; proof in DESIGN.md, "Exactness of the
-filter").  tests/filter_check/filter_check.c draws random and adversarial
+mt_pass / mt_pass3 and the per-ray precomputed plk_pass in binary32;
+proofs in DESIGN.md, "Exactness of the filter" and "The per-ray filter").  tests/filter_check/filter_check.c draws random and adversarial
 rays (edges, vertices, grazing, best at the hit distance); a tightened
 filter mutant shows violations, so the harness is sensitive."""
 import os
@@ -22,16 +22,18 @@ def checker(tmp_path_factory):
 
 def _run(exe, n, seed):
     out = subprocess.run([exe, str(n), str(seed)], check=True, capture_output=True, text=True).stdout
-    pairs, accepts, bad_old, bad_new, p_old, p_new = map(int, out.split())
-    return pairs, accepts, bad_old, bad_new, p_old, p_new
+    pairs, accepts, bad_old, bad_new, p_old, p_new, bad_plk, p_plk = map(int, out.split())
+    return pairs, accepts, bad_old, bad_new, p_old, p_new, bad_plk, p_plk
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_filters_conservative(checker, seed):
-    pairs, accepts, bad_old, bad_new, p_old, p_new = _run(checker, 3_000_000, seed)
+    pairs, accepts, bad_old, bad_new, p_old, p_new, bad_plk, p_plk = _run(checker, 3_000_000, seed)
     assert accepts > pairs // 20          # the adversarial draws do reach the accept region
     assert bad_old == 0 and bad_new == 0  # no accepted pair is filtered out
+    assert bad_plk == 0
     assert p_new <= p_old * 1.01          # and the new form filters as much as the old one
+    assert p_plk < pairs                  # the per-ray filter does reject (its margin is not everything)
 
 
 def test_harness_detects_a_wrong_filter(tmp_path):
@@ -46,5 +48,18 @@ def test_harness_detects_a_wrong_filter(tmp_path):
     p.write_text(mutant)
     exe = str(tmp_path / "mut")
     subprocess.run(["gcc", "-O2", "-std=c11", "-ffp-contract=off", "-o", exe, str(p), "-lm"], check=True)
-    _, _, bad_old, bad_new, _, _ = _run(exe, 3_000_000, 1)
+    _, _, bad_old, bad_new, _, _, _, _ = _run(exe, 3_000_000, 1)
     assert bad_old == 0 and bad_new > 0
+
+
+def test_harness_detects_a_plk_threshold_without_margin(tmp_path):
+    """plk_pass with T = 0 (no error margin) filters out accepted pairs."""
+    src = open(SRC).read()
+    old = "const float T = fmaf(0x1p-13f, O + A, 0x1p-40f);"
+    assert old in src
+    p = tmp_path / "mut.c"
+    p.write_text(src.replace(old, "const float T = 0.0f;"))
+    exe = str(tmp_path / "mut")
+    subprocess.run(["gcc", "-O2", "-std=c11", "-ffp-contract=off", "-o", exe, str(p), "-lm"], check=True)
+    _, _, _, _, _, _, bad_plk, _ = _run(exe, 3_000_000, 1)
+    assert bad_plk > 0
