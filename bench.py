@@ -58,6 +58,25 @@ def parse():
     return ap.parse_args()
 
 
+def launched_kernel(rt2, scene, traversal):
+    """Kernel + variant of the scene's last launch (the auto choice depends on
+    the slab size: rank slabs at N > 1 take other variants than the full image)."""
+    import ctypes as C
+    c = (C.c_ulonglong * 8)()
+    lv = C.c_int(-1)
+    rt2.lib().rt2_scene_diag(scene._p, c, C.byref(lv))
+    name = rt2.lib().rt2_variant_name(lv.value) if lv.value >= 0 else None
+    if not name:
+        return KERNEL_NAMES[traversal]
+    name = name.decode()
+    kern = {"smem": "render_smem", "split": "render_split", "tiled": "render_tiled", "resident": "render_resident",
+            "bvh3": "render_bvh3", "bvh2": "render_bvh2", "bvh": "render_bvh"}
+    for prefix, k in kern.items():
+        if name.startswith(prefix):
+            return f"{k} (rt2_render.hip, variant {name})"
+    return name
+
+
 def cpu_baseline(sd, spec, u, gpu_image, threads):
     """Times oracle/ (CPU restatement of compute.glsl) on a strided pixel sample
     (every k-th pixel in raster order, full spp) and checks the GPU's pixels
@@ -170,6 +189,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     st = scene.stats(reset=True)
+    kernel_name = launched_kernel(rt2, scene, args.traversal)
     t = torch.tensor([elapsed, kern_ms, float(st.tests), float(st.segments), float(st.node_visits)],
                      dtype=torch.float64, device="cuda")
     if world > 1:
@@ -215,7 +235,7 @@ def main():
                    "tile_rows": args.tile_rows},
         "roofline": {"bound": "valu", "achieved": round(flops, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(flops / VALU_PEAK_TFLOPS, 4), "traffic": None,
-                     "kernel": KERNEL_NAMES[args.traversal], "kernel_ms": round(kern_ms, 3),
+                     "kernel": kernel_name, "kernel_ms": round(kern_ms, 3),
                      "tests_per_launch": int(tests_per_launch),
                      "node_visits_per_launch": int(visits_per_launch),
                      "flop_model": "53 x ray-triangle tests + 24 x BVH interior visits (2 slab boxes)",
@@ -259,7 +279,7 @@ def main():
         out["alt_traversal"] = {
             "traversal": alt, "value": round(samples_per_step * args.steps / el2 / 1e6, 3),
             "ms_per_step": round(el2 / args.steps * 1e3, 3),
-            "kernel": KERNEL_NAMES[alt],
+            "kernel": launched_kernel(rt2, scene, alt),
             "kernel_ms": round(float(np.mean([a.elapsed_time(b) for a, b in ev2])), 3),
             "segments_per_sample": round(st2.segments / (samples_per_step * args.steps), 4),
             "tests_per_segment": round(st2.tests / max(st2.segments, 1), 3),

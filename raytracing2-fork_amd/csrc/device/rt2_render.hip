@@ -556,6 +556,7 @@ constexpr size_t kResidentMaxBytes = 112 * 1024;
 constexpr int kSmemMaxTris = 16384;
 constexpr int kDefaultBvhVariant = 53;
 constexpr int kSmallSlabVariant = 85;  // split4/max3f8/w6: brute force on slabs with fewer items than lanes
+constexpr int kMidSlabVariant = 67;    // smem/256/max3f8/coop32 (5 waves/SIMD): 1 to 4 items per lane
 }  // namespace
 
 extern "C" const char* rt2_variant_name(int v) { return v >= 0 && v < kNumVariants ? kVariants[v].name : nullptr; }
@@ -735,15 +736,26 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
         if (vi <= 0 || vi >= kNumVariants || kVariants[vi].kind >= K_BVH) {
             vi = s->n_tris <= kSmemMaxTris ? 0 : 2;
             if (vi == 0) {
-                // fewer items than resident lanes (a 1/8 slab of config B: 259k
-                // pixels, 393k lanes): every lane owns at most one long item and
-                // the launch is its tail; the split-wave kernel traces each 64
-                // rays with S waves (1/S of the triangles each)
-                int occ0 = 0;
-                HIPCHECK(kVariants[0].occupancy(&occ0, 0));
-                const unsigned long long lanes =
-                    (unsigned long long)s->num_cus * (unsigned long long)std::max(occ0, 1) * kVariants[0].block;
-                if (p.n_items < lanes) vi = kSmallSlabVariant;
+                // items per resident lane decide the tail: a lane ends on a
+                // whole item, so with few items per lane the last round runs
+                // partly empty.  >= 4 per lane at 6 waves/SIMD (a full config B
+                // image): the 6-wave kernel; fewer: the 5-wave kernel (1/2 and
+                // 1/4 slabs: 3-4 % faster than 6 waves there); fewer items than
+                // 5-wave lanes (a 1/8 slab: 259k pixels, 327k lanes): every lane
+                // owns at most one long item, so the split-wave kernel traces
+                // each 64 rays with S waves (1/S of the triangles each)
+                auto lanes = [&](int v, unsigned long long& out) -> int {
+                    int occ0 = 0;
+                    HIPCHECK(kVariants[v].occupancy(&occ0, 0));
+                    out = (unsigned long long)s->num_cus * (unsigned long long)std::max(occ0, 1) * kVariants[v].block;
+                    return 0;
+                };
+                unsigned long long lanes6 = 0, lanes5 = 0;
+                if (lanes(0, lanes6) < 0 || lanes(kMidSlabVariant, lanes5) < 0) return -1;
+                if (p.n_items < lanes5)
+                    vi = kSmallSlabVariant;
+                else if (p.n_items < 4 * lanes6)
+                    vi = kMidSlabVariant;
             }
         }
         if (kVariants[vi].kind == K_RESIDENT && !fits) vi = 2;  // a resident variant cannot hold this scene
