@@ -418,6 +418,7 @@ struct Variant {
     int block;
     hipError_t (*launch)(const RenderParams&, int blocks, size_t lds, hipStream_t st);
     hipError_t (*occupancy)(int* occ, size_t lds);
+    const void* (*kernel)();
     const char* name;
 };
 
@@ -442,26 +443,27 @@ hipError_t launch_t(const RenderParams& p, int blocks, size_t lds, hipStream_t s
     return hipGetLastError();
 }
 template <int KIND, int BLOCK, int MT, int UNROLL>
-hipError_t occ_t(int* occ, size_t lds) {
+const void* kptr_t() {
     if constexpr (KIND == K_TILED)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_tiled<BLOCK, MT, UNROLL>, BLOCK, lds);
+        return reinterpret_cast<const void*>(render_tiled<BLOCK, MT, UNROLL>);
     else if constexpr (KIND == K_SMEM)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_smem<BLOCK, MT % 1000, MT / 1000, UNROLL>,
-                                                            BLOCK, 0);
+        return reinterpret_cast<const void*>(render_smem<BLOCK, MT % 1000, MT / 1000, UNROLL>);
     else if constexpr (KIND == K_SPLIT)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            occ, render_split<BLOCK / 64, MT % 1000, MT / 1000, UNROLL>, BLOCK, 0);
+        return reinterpret_cast<const void*>(render_split<BLOCK / 64, MT % 1000, MT / 1000, UNROLL>);
     else if constexpr (KIND == K_BVH)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_bvh<BLOCK>, BLOCK, lds);
+        return reinterpret_cast<const void*>(render_bvh<BLOCK>);
     else if constexpr (KIND == K_BVH2)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_bvh2<BLOCK, MT>, BLOCK, lds);
+        return reinterpret_cast<const void*>(render_bvh2<BLOCK, MT>);
     else if constexpr (KIND == K_BVH3)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            occ, render_bvh3<BLOCK, MT % 1000, (MT / 1000) % 10, UNROLL, MT / 10000>, BLOCK, lds);
+        return reinterpret_cast<const void*>(render_bvh3<BLOCK, MT % 1000, (MT / 1000) % 10, UNROLL, MT / 10000>);
     else
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, render_resident<BLOCK, MT, UNROLL>, BLOCK, lds);
+        return reinterpret_cast<const void*>(render_resident<BLOCK, MT, UNROLL>);
 }
-#define RT2_VARIANT(T, B, M, U, NAME) Variant{T, B, launch_t<T, B, M, U>, occ_t<T, B, M, U>, NAME}
+template <int KIND, int BLOCK, int MT, int UNROLL>
+hipError_t occ_t(int* occ, size_t lds) {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, kptr_t<KIND, BLOCK, MT, UNROLL>(), BLOCK, lds);
+}
+#define RT2_VARIANT(T, B, M, U, NAME) Variant{T, B, launch_t<T, B, M, U>, occ_t<T, B, M, U>, kptr_t<T, B, M, U>, NAME}
 
 const Variant kVariants[] = {
     RT2_VARIANT(K_SMEM, 256, 32508, 6, "smem/256/max3f8/coop32/w6"), // 0: default (<= kSmemMaxTris)
@@ -560,6 +562,20 @@ constexpr int kMidSlabVariant = 67;    // smem/256/max3f8/coop32 (5 waves/SIMD):
 }  // namespace
 
 extern "C" const char* rt2_variant_name(int v) { return v >= 0 && v < kNumVariants ? kVariants[v].name : nullptr; }
+
+// Not in rt2.h (diagnostics): the occupancy API's blocks per CU and the
+// kernel's register counts (hipFuncGetAttributes) for variant v.
+extern "C" int rt2_variant_occupancy(int v, int* api_blocks, int* num_regs, int* local_bytes) {
+    if (v < 0 || v >= kNumVariants) return -1;
+    int occ = 0;
+    HIPCHECK(kVariants[v].occupancy(&occ, 0));
+    hipFuncAttributes a;
+    HIPCHECK(hipFuncGetAttributes(&a, kVariants[v].kernel()));
+    if (api_blocks) *api_blocks = occ;
+    if (num_regs) *num_regs = a.numRegs;
+    if (local_bytes) *local_bytes = (int)a.localSizeBytes;
+    return 0;
+}
 
 extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_begin, uint32_t frame_count,
                           rt2_shard sh, float* d_accum, uint32_t* d_accum8, void* stream) {
