@@ -83,7 +83,9 @@ __global__ __launch_bounds__(BLOCK) void render_tiled(RenderParams p) {
             for (int i = threadIdx.x; i < 3 * cnt; i += BLOCK) lds[i] = p.tri[3 * base + i];
             __syncthreads();
             if (tracing) {
-                if constexpr (MT >= 100) {
+                if constexpr (MT >= 500) {
+                    sweep_masked<MT - 500, false, 1>(o, d, lds, nullptr, cnt, base, best, bi, bestK);
+                } else if constexpr (MT >= 100) {
                     sweep_masked<MT - 100, false>(o, d, lds, nullptr, cnt, base, best, bi, bestK);
                 } else if constexpr (MT >= 2) {
                     sweep_grouped<MT>(o, d, lds, cnt, base, best, bi, bestK);

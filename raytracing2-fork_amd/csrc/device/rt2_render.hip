@@ -468,7 +468,7 @@ hipError_t occ_t(int* occ, size_t lds) {
 const Variant kVariants[] = {
     RT2_VARIANT(K_SMEM, 256, 32508, 6, "smem/256/max3f8/coop32/w6"), // 0: default (<= kSmemMaxTris)
     RT2_VARIANT(K_RESIDENT, 256, 0, 4, "resident/256/plain/u4"),     // 1: round-1 v1 kernel
-    RT2_VARIANT(K_TILED, 512, 4, 1, "tiled/512/grouped4"),           // 2: default (large scenes)
+    RT2_VARIANT(K_TILED, 512, 4, 1, "tiled/512/grouped4"),           // 2: round-1 large-scene default
     RT2_VARIANT(K_RESIDENT, 256, 1, 4, "resident/256/filtered/u4"),  // 3
     RT2_VARIANT(K_RESIDENT, 1024, 1, 4, "resident/1024/filtered/u4"),// 4
     RT2_VARIANT(K_RESIDENT, 512, 1, 4, "resident/512/filtered/u4"),  // 5
@@ -552,12 +552,17 @@ const Variant kVariants[] = {
     RT2_VARIANT(K_SPLIT, 512, 8, 4, "split8/masked8/w4"),            // 83
     RT2_VARIANT(K_SPLIT, 512, 1008, 4, "split8/max3f8/w4"),          // 84
     RT2_VARIANT(K_SPLIT, 256, 1008, 6, "split4/max3f8/w6"),          // 85
+    RT2_VARIANT(K_TILED, 512, 504, 1, "tiled/512/max3f4"),           // 86: default (large scenes)
+    RT2_VARIANT(K_TILED, 512, 508, 1, "tiled/512/max3f8"),           // 87
+    RT2_VARIANT(K_TILED, 256, 508, 1, "tiled/256/max3f8"),           // 88
+    RT2_VARIANT(K_TILED, 1024, 504, 1, "tiled/1024/max3f4"),         // 89
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr size_t kResidentMaxBytes = 112 * 1024;
 constexpr int kSmemMaxTris = 16384;
 constexpr int kDefaultBvhVariant = 53;
 constexpr int kSmallSlabVariant = 85;  // split4/max3f8/w6: brute force on slabs with fewer items than lanes
+constexpr int kLargeSceneVariant = 86;  // tiled/512/max3f4: LDS tiles above kSmemMaxTris triangles
 constexpr int kMidSlabVariant = 67;    // smem/256/max3f8/coop32 (5 waves/SIMD): 1 to 4 items per lane
 }  // namespace
 
@@ -750,7 +755,7 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
             vi = kDefaultBvhVariant;
     } else {
         if (vi <= 0 || vi >= kNumVariants || kVariants[vi].kind >= K_BVH) {
-            vi = s->n_tris <= kSmemMaxTris ? 0 : 2;
+            vi = s->n_tris <= kSmemMaxTris ? 0 : kLargeSceneVariant;
             if (vi == 0) {
                 // items per resident lane decide the tail: a lane ends on a
                 // whole item, so with few items per lane the last round runs
@@ -774,7 +779,7 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
                     vi = kMidSlabVariant;
             }
         }
-        if (kVariants[vi].kind == K_RESIDENT && !fits) vi = 2;  // a resident variant cannot hold this scene
+        if (kVariants[vi].kind == K_RESIDENT && !fits) vi = kLargeSceneVariant;  // cannot hold this scene
     }
     const Variant& V = kVariants[vi];
     size_t lds = 0;

@@ -259,7 +259,7 @@ def test_frame_split_identical(rt2mod, oraclemod, config_scene, torch_cuda, trav
 # brute-force kernel variants that change the schedule, not the arithmetic:
 # masked/ballot/min-filter sweeps, cooperative and team tail modes, occupancy hints
 BRUTE_VARIANTS = [0, 1, 2, 22, 24, 28, 31, 52, 59, 60, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73,
-                  74, 75, 76, 77, 78, 79, 80, 83, 84, 85]
+                  74, 75, 76, 77, 78, 79, 80, 83, 84, 85, 86, 87, 88, 89]
 PLK_VARIANTS = [74, 76, 79, 80]
 
 
