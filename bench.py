@@ -144,8 +144,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        # nccl = RCCL over xGMI (one rank per GPU).  RT2_BENCH_BACKEND=gloo is a
+        # rehearsal mode for boxes with fewer GPUs than ranks (ranks share
+        # devices, collectives staged through host memory); never the measured
+        # configuration.
+        backend = os.environ.get("RT2_BENCH_BACKEND", "nccl")
+        local = local % max(torch.cuda.device_count(), 1) if backend == "gloo" else local
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
@@ -246,7 +255,7 @@ def main():
         "cpu_baseline": None,
     }
     traffic_file = os.path.join(ROOT, "profiles", f"pmc_config{spec.name}.json")
-    if os.path.exists(traffic_file):
+    if world == 1 and os.path.exists(traffic_file):  # PMC traffic was measured for the 1-GPU launch
         with open(traffic_file) as f:
             out["roofline"]["traffic"] = json.load(f).get("hbm_bytes_per_launch")
     alt = "bvh" if args.traversal == "brute" else "brute"

@@ -51,6 +51,9 @@ def gather_image(slab, height: int, width: int, tile_rows: int, rank: int, nrank
     import torch
     import torch.distributed as dist
     mr = max_slab_rows(height, tile_rows, nranks)
+    dev = slab.device
+    if slab.is_cuda and dist.get_backend(group) == "gloo":
+        slab = slab.cpu()  # gloo collectives take host tensors
     if slab.shape[0] == mr:
         padded = slab.contiguous()
     else:
@@ -59,7 +62,7 @@ def gather_image(slab, height: int, width: int, tile_rows: int, rank: int, nrank
     if rank == root:
         gathered = torch.empty((nranks,) + tuple(padded.shape), dtype=slab.dtype, device=slab.device)
         dist.gather(padded, gather_list=list(gathered.unbind(0)), dst=root, group=group)
-        return assemble(gathered, height, width, tile_rows, nranks)
+        return assemble(gathered, height, width, tile_rows, nranks).to(dev)
     dist.gather(padded, gather_list=None, dst=root, group=group)
     return None
 
