@@ -428,7 +428,7 @@ __device__ __forceinline__ void bvh_interior3(TravState3& T, int* st, int e, con
         // arithmetics: that axis puts the same t into tMin's max and tMax's min
         const bool flatA = (r0.x == r0.w) | (r0.y == r1.x) | (r0.z == r1.y);
         const bool flatB = (r1.z == r2.y) | (r1.w == r2.z) | (r2.x == r2.w);
-        bool amb = (near_tie(aMin, aMax) & !flatA) | (near_tie(bMin, bMax) & !flatB);
+        bool amb = (int)(near_tie(aMin, aMax) & !flatA) | (int)(near_tie(bMin, bMax) & !flatB);  // branch-free
         amb |= hitA & hitB & near_tie(dA, dB);
         amb |= hitA & near_tie(dA, T.best);
         amb |= hitB & near_tie(dB, T.best);
