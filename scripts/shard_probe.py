@@ -19,11 +19,14 @@ ap.add_argument("--traversal", default="brute")
 ap.add_argument("--tile-rows", type=int, default=1)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--variants", default="0")
+ap.add_argument("--cost-order", type=int, default=-1, help="1/0: most-expensive-first item order on/off")
 a = ap.parse_args()
 sd, spec = rt2.build_config_scene(a.config)
 u = rt2.offline_uniforms(spec.width, spec.height, spec.bounces, spec.rays, sd.num_triangles)
 scene = rt2.Scene(sd, 0)
 scene.set_traversal(a.traversal)
+if a.cost_order >= 0:
+    scene.set_cost_order(bool(a.cost_order))
 
 
 def slab_time(sh):
@@ -46,7 +49,7 @@ for var in [int(v) for v in a.variants.split(",")]:
     scene.set_variant(var)
     out = {n: slab_time(rt2.shard(a.tile_rows, 0, n)) for n in (1, 2, 4, 8)}
     base = out[1]
-    print(json.dumps({"config": a.config, "traversal": a.traversal, "tile_rows": a.tile_rows, "variant": var,
+    print(json.dumps({"config": a.config, "traversal": a.traversal, "tile_rows": a.tile_rows, "variant": var, "cost_order": a.cost_order,
                       "name": rt2.lib().rt2_variant_name(var).decode() if var else "auto",
                       "slab_ms": {n: round(t * 1e3, 2) for n, t in out.items()},
                       "predicted_efficiency": {n: round(base / n / t, 3) for n, t in out.items()}}), flush=True)
