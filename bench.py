@@ -258,6 +258,13 @@ def main():
     if world == 1 and os.path.exists(traffic_file):  # PMC traffic was measured for the 1-GPU launch
         with open(traffic_file) as f:
             out["roofline"]["traffic"] = json.load(f).get("hbm_bytes_per_launch")
+        if out["roofline"]["traffic"]:
+            # rocprof-measured HBM bandwidth of the launch (PMC bytes / this run's kernel time)
+            gbs = out["roofline"]["traffic"] / (kern_ms * 1e-3) / 1e9
+            out["roofline"]["hbm_measured"] = {"achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                               "frac": round(gbs / HBM_PEAK_GBS, 4),
+                                               "source": f"profiles/pmc_config{spec.name}.json (FETCH_SIZE x2 + "
+                                                         f"WRITE_SIZE, MI355X_MICROARCH.md HBM section)"}
     alt = "bvh" if args.traversal == "brute" else "brute"
     # brute force over 100k+ triangles takes minutes per step: not timed beside BVH there
     if world == 1 and not args.no_alt and (alt == "bvh" or sd.num_triangles <= 20000):
