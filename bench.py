@@ -261,7 +261,7 @@ def main():
         if out["roofline"]["traffic"]:
             # rocprof-measured HBM bandwidth of the launch (PMC bytes / this run's kernel time)
             gbs = out["roofline"]["traffic"] / (kern_ms * 1e-3) / 1e9
-            out["roofline"]["hbm_measured"] = {"achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            out["roofline"]["hbm_measured"] = {"achieved": round(gbs, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                                "frac": round(gbs / HBM_PEAK_GBS, 4),
                                                "source": f"profiles/pmc_config{spec.name}.json (FETCH_SIZE x2 + "
                                                          f"WRITE_SIZE, MI355X_MICROARCH.md HBM section)"}

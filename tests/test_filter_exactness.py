@@ -38,10 +38,10 @@ def test_filters_conservative(checker, seed):
 
 def test_harness_detects_a_wrong_filter(tmp_path):
     src = open(SRC).read()
-    old = "return fmaxf(fmaxf(fmaxf(q.U, -q.V), X), fmaxf(-q.tnum, Y)) <= B;"
+    old = "return fmaxf(fmaxf(fmaxf(fmaxf(q.U, -q.V), X), -q.tnum), Y) <= B;"
     assert old in src
-    mutant = src.replace(old, "return fmaxf(fmaxf(fmaxf(q.U, -q.V), fmaf(-q.det, 1.0f, q.V - q.U)), "
-                              "fmaxf(-q.tnum, fmaf(-q.det, best_plain(bestK), q.tnum))) <= 0.0f;")
+    mutant = src.replace(old, "return fmaxf(fmaxf(fmaxf(fmaxf(q.U, -q.V), fmaf(-q.det, 1.0f, q.V - q.U)), "
+                              "-q.tnum), fmaf(-q.det, best_plain(bestK), q.tnum)) <= 0.0f;")
     mutant = mutant.replace("static int pass_new(", "static float best_plain(float k) { return k / 1.0009765625f; }\n"
                                                     "static int pass_new(")
     p = tmp_path / "mut.c"
