@@ -470,7 +470,7 @@ __device__ __forceinline__ void bvh_leaf3(TravState3& T, int e, const rt2_node* 
     for (int i = start; i < start + cnt; i++) {
         const float4* t = tri + 3 * i;
         const MtQ q = mt_quantities(T.R.o, T.R.d, t[0], t[1], t[2]);
-        if (mt_pass(q, T.bestK)) mt_exact(q, i, T.best, T.bi, T.bestK);
+        if (mt_pass3(q, T.bestK)) mt_exact(q, i, T.best, T.bi, T.bestK);
     }
 }
 

@@ -588,7 +588,7 @@ __device__ __forceinline__ void coop_closest(const f3& o, const f3& d, const flo
     for (int i = lane; i < n; i += 64) {
         const float4* t = tris + 3 * i;
         const MtQ q = mt_quantities(o, d, t[0], t[1], t[2]);
-        if (mt_pass(q, bestK)) mt_exact(q, i, best, bi, bestK);
+        if (mt_pass3(q, bestK)) mt_exact(q, i, best, bi, bestK);
     }
     for (int off = 32; off > 0; off >>= 1) {
         const float ob = __shfl_xor(best, off);
