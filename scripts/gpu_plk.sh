@@ -4,5 +4,5 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "plk or brute_variants" > gpurun_out/gpu_plk_tests.log 2>&1 || { echo "plk tests failed"; exit 1; }
-timeout -k 10 240 python scripts/ab_variants.py --variants 0,90,0,90,28 --rounds 3 > gpurun_out/ab_plk.json 2>&1 || { echo "ab failed"; exit 1; }
+timeout -k 10 240 python scripts/ab_variants.py --variants 0,90,91,0,90,91 --rounds 2 > gpurun_out/ab_plk.json 2>&1 || { echo "ab failed"; exit 1; }
 echo "all ok"
