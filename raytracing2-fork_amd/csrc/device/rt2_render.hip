@@ -281,6 +281,9 @@ extern "C" int rt2_scene_set_traversal(rt2_scene* s, int traversal) {
     return 0;
 }
 
+static int scene_init(rt2_scene* s, const rt2_triangle* tris, int32_t n_tris, const rt2_material* mats,
+                      int32_t n_mats, const rt2_node* nodes, int32_t n_nodes, int32_t device);
+
 extern "C" int rt2_scene_create(const rt2_triangle* tris, int32_t n_tris, const rt2_material* mats, int32_t n_mats,
                                 const rt2_node* nodes, int32_t n_nodes, int32_t device, rt2_scene** out) {
     if (!out || n_tris < 0 || n_mats < 1 || !mats || (n_tris > 0 && !tris)) {
@@ -302,6 +305,18 @@ extern "C" int rt2_scene_create(const rt2_triangle* tris, int32_t n_tris, const 
     }
     HIPCHECK(hipSetDevice(device));
     rt2_scene* s = new rt2_scene();
+    if (scene_init(s, tris, n_tris, mats, n_mats, nodes, n_nodes, device) != 0) {
+        rt2_scene_destroy(s);  // frees whatever was allocated before the failure
+        return -1;
+    }
+    *out = s;
+    return 0;
+}
+
+// Uploads and derived device arrays of rt2_scene_create; on failure returns
+// -1 with the error set and leaves the partial scene to the caller to destroy.
+static int scene_init(rt2_scene* s, const rt2_triangle* tris, int32_t n_tris, const rt2_material* mats,
+                      int32_t n_mats, const rt2_node* nodes, int32_t n_nodes, int32_t device) {
     s->device = device;
     s->n_tris = n_tris;
     s->n_mats = n_mats;
@@ -325,7 +340,6 @@ extern "C" int rt2_scene_create(const rt2_triangle* tris, int32_t n_tris, const 
         if (s->bvh_depth < 0 || s->bvh_depth > 62) {
             if (s->bvh_depth > 62) err = "BVH deeper than compute.glsl's 64-entry stack";
             rt2h::set_error("rt2_scene_create: bad node array: " + err);
-            delete s;
             return -1;
         }
         HIPCHECK(hipMalloc(&s->d_nodes, (size_t)n_nodes * sizeof(rt2_node)));
@@ -333,7 +347,6 @@ extern "C" int rt2_scene_create(const rt2_triangle* tris, int32_t n_tris, const 
         std::vector<float4> rec;
         if (bvh_records(nodes, n_nodes, rec, s->bvh_root, err) < 0) {
             rt2h::set_error("rt2_scene_create: bad node array: " + err);
-            delete s;
             return -1;
         }
         // the first three float4 of a record are box coordinates (the 4th: stack entries)
@@ -351,20 +364,19 @@ extern "C" int rt2_scene_create(const rt2_triangle* tris, int32_t n_tris, const 
                            s->d_mtl);
         HIPCHECK(hipGetLastError());
         HIPCHECK(hipMalloc(&s->d_plk, nt * 4 * sizeof(float4)));
-        uint32_t* d_flags = nullptr;
-        HIPCHECK(hipMalloc(&d_flags, 2 * sizeof(uint32_t)));
+        // two scratch words in an unused counter slot (zeroed again below)
+        uint32_t* d_flags = reinterpret_cast<uint32_t*>(s->d_counters + kCounters - 2);
         HIPCHECK(hipMemset(d_flags, 0, 2 * sizeof(uint32_t)));
         hipLaunchKernelGGL(prep_plk, dim3((n_tris + 255) / 256), dim3(256), 0, 0, s->d_tri, n_tris, s->d_plk, d_flags);
         HIPCHECK(hipGetLastError());
         uint32_t flags[2];
         HIPCHECK(hipMemcpy(flags, d_flags, sizeof(flags), hipMemcpyDeviceToHost));
-        HIPCHECK(hipFree(d_flags));
+        HIPCHECK(hipMemset(d_flags, 0, 2 * sizeof(uint32_t)));
         s->plk_outside = (int)flags[0];
         s->plk_ok = (unsigned long long)flags[0] * 64 <= (unsigned long long)n_tris;  // <= 1/64 always-pass records
         std::memcpy(&s->plk_A, &flags[1], sizeof(float));
     }
     HIPCHECK(hipDeviceSynchronize());
-    *out = s;
     return 0;
 }
 
