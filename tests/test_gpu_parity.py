@@ -90,6 +90,32 @@ def test_config_B_full_size_rows_exact(rt2mod, oraclemod, config_scene, torch_cu
     assert np.sqrt((d ** 2).mean()) < RMSE_TOL
 
 
+def _last_variant(rt2mod, scene):
+    import ctypes as C
+    c = (C.c_ulonglong * 8)()
+    lv = C.c_int(-1)
+    assert rt2mod.lib().rt2_scene_diag(scene._p, c, C.byref(lv)) == 0
+    return rt2mod.lib().rt2_variant_name(lv.value).decode()
+
+
+def test_auto_variant_by_items_per_lane(rt2mod, config_scene, torch_cuda):
+    """The launcher picks the brute kernel by items per resident lane (DESIGN.md
+    §Kernels): the 6-wave kernel for the full config B image, the 5-wave kernel
+    for a 1/2 slab, the split-wave kernel for a 1/8 slab — and every slab is
+    bit-identical to the same rows of the full image."""
+    sd, spec = config_scene("B")
+    u = rt2mod.offline_uniforms(spec.width, spec.height, spec.bounces, spec.rays, sd.num_triangles)
+    scene = rt2mod.Scene(sd, 0)
+    full = scene.render_host(u, 0, 1)
+    assert _last_variant(rt2mod, scene) == "smem/256/max3f8/coop32/w6"
+    for n, want in ((2, "smem/256/max3f8/coop32"), (8, "split4/max3f8/w6")):
+        sh = rt2mod.shard(1, n - 1, n)
+        img = scene.render_host(u, 0, 1, sh)
+        assert _last_variant(rt2mod, scene) == want
+        rows = rt2mod.shard_row_ids(spec.height, sh)
+        assert np.array_equal(img, full[rows]), f"1/{n} slab differs from the full image"
+
+
 def test_frames_split_across_calls_bit_identical(rt2mod, config_scene, torch_cuda):
     torch = torch_cuda
     sd, spec = config_scene("A")
