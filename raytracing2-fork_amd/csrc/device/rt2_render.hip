@@ -571,7 +571,7 @@ const Variant kVariants[] = {
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr size_t kResidentMaxBytes = 112 * 1024;
-constexpr int kSmemMaxTris = 16384;
+constexpr int kSmemMaxTris = 131072;  // scalar path up to 6.3 MB of records (config C: 781 vs 817 ms tiled; config E: tiled 1,704 vs 2,312 ms)
 constexpr int kDefaultBvhVariant = 53;
 constexpr int kSmallSlabVariant = 85;  // split4/max3f8/w6: brute force on slabs with fewer items than lanes
 constexpr int kLargeSceneVariant = 86;  // tiled/512/max3f4: LDS tiles above kSmemMaxTris triangles

@@ -218,7 +218,8 @@ def test_defocus_and_frame_wrap(rt2mod, oraclemod, config_scene, torch_cuda):
 
 
 def test_tiled_kernel_exact(rt2mod, oraclemod, config_scene, torch_cuda):
-    """The LDS-tiled sweep (forced on a small scene, and automatic on 100k triangles)."""
+    """The LDS-tiled sweep (the automatic choice above 131,072 triangles), forced
+    on config B and on config C's 100k triangles."""
     sd, spec = config_scene("B")
     u = rt2mod.offline_uniforms(96, 54, 8, 4, sd.num_triangles)
     scene = rt2mod.Scene(sd, 0)
@@ -231,6 +232,7 @@ def test_tiled_kernel_exact(rt2mod, oraclemod, config_scene, torch_cuda):
     assert sdc.num_triangles == 100016
     u = rt2mod.offline_uniforms(24, 14, 8, 2, sdc.num_triangles)
     scene = rt2mod.Scene(sdc, 0)
+    scene.set_variant(86)
     img = scene.render_host(u, 0, 1)
     ref, _, _ = oracle_mean(oraclemod, sdc, u, np.arange(14), 0, 1, "bvh")
     d = np.abs(img[..., :3] - ref)
