@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X render path on BASELINE.json's metric.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config B] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config B] [--traversal brute|bvh]
+                    [--no-cpu-baseline] [--no-alt] [--no-config-c]
 
 One "step" = one render of the configuration's image (config B: campfire +
 Cornell box, 1920x1080, 64 rays/pixel x 1 frame, 8 bounces) —
@@ -12,18 +13,28 @@ uploaded to HBM before the timed region.  For N > 1 the driver launches one
 process per GPU through torch.distributed.run.
 
 Prints ONE JSON line (rank 0):
-  value       Msamples/s of the whole job = W*H*R*F*K / max-over-ranks wall time
-  roofline    dominant kernel (the render kernel), FP32-VALU-bound: algorithmic
-              FLOP = 53 x ray-triangle tests per launch / the
-              launch's average HIP-event duration, against 157.3 TFLOP/s; plus
-              the north star's HBM-read figure (36 B x tests) against 8 TB/s
+  value         Msamples/s of the whole job = W*H*R*F*K / max-over-ranks wall time
+  roofline      dominant kernel (the render kernel), FP32-VALU-bound: algorithmic
+                FLOP = 53 x ray-triangle tests per launch / the
+                launch's average HIP-event duration, against 157.3 TFLOP/s; plus
+                the north star's HBM-read figure (36 B x tests) against 8 TB/s.
+                `traffic` = PMC-measured HBM bytes per launch from
+                profiles/pmc_config<X>.json, attached only when that profile was
+                taken of the same kernel variant built from the same kernel sources
   cpu_baseline  the CPU restatement of compute.glsl (oracle/, reference-faithful
-              BVH traversal) on the host cores, on a bounded strided pixel sample
-              (every k-th pixel in raster order, full spp); the brute-force CPU
-              rate is reported beside it
-  parity      GPU pixels vs the CPU oracle on those same sampled pixels
+                BVH traversal) on the host CPUs this job may use (the cgroup CPU
+                quota of a GPU box), on a bounded evenly spread pixel sample at
+                full spp; the brute-force CPU rate beside it; the host's model,
+                core counts and a linear extrapolation to every core of the node
+  parity        GPU pixels vs the CPU oracle on those same sampled pixels
+  config_C      (1 GPU, config B runs) the north-star target configuration
+                (100k triangles, 1920x1080, 256 spp): one brute-force step with
+                its own roofline, the BVH kernel, the CPU baseline, parity, and
+                whether the >= 10x target is met and by which kernel
 """
 import argparse
+import glob
+import hashlib
 import json
 import os
 import sys
@@ -38,8 +49,9 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec
 FLOP_PER_TEST = 53
 FLOP_PER_VISIT = 24        # BVH interior node: 2 boxes x (6 sub + 6 div), compute.glsl:382-408
 BYTES_PER_TEST = 36        # a, b, c positions
-KERNEL_NAMES = {"brute": "render_smem (rt2_render.hip, variant smem/256/max3f8/coop32/w6)",
-                "bvh": "render_bvh3 (rt2_render.hip, variant bvh3/256/t16/w5)"}
+TARGET_RATIO = 10.0        # north star: >= 10x the CPU reference at config C on 1 GPU
+KERNEL_FILES = {"smem": "render_smem", "split": "render_split", "tiled": "render_tiled",
+                "resident": "render_resident", "bvh3": "render_bvh3", "bvh2": "render_bvh2", "bvh": "render_bvh"}
 
 
 def parse():
@@ -54,85 +66,238 @@ def parse():
                     help="brute = the north-star kernel (default); bvh = the reference's traversal on the GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-alt", action="store_true", help="skip timing the other traversal beside the headline")
+    ap.add_argument("--no-config-c", action="store_true", help="skip the config C (north-star target) leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target seconds per CPU baseline mode")
     return ap.parse_args()
 
 
-def launched_kernel(rt2, scene, traversal):
-    """Kernel + variant of the scene's last launch (the auto choice depends on
-    the slab size: rank slabs at N > 1 take other variants than the full image)."""
+def kernel_source_digest():
+    """sha256 over the device sources compiled into the render kernels; a PMC
+    profile carries the digest of the sources it was measured on."""
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "raytracing2-fork_amd", "csrc", "device", "*")))
+    files.append(os.path.join(ROOT, "include", "rt2_pinned_math.h"))
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def launched_variant(rt2, scene):
+    """Name of the kernel variant of the scene's last launch (the automatic
+    choice depends on the slab size: rank slabs at N > 1 take other variants)."""
     import ctypes as C
     c = (C.c_ulonglong * 8)()
     lv = C.c_int(-1)
     rt2.lib().rt2_scene_diag(scene._p, c, C.byref(lv))
     name = rt2.lib().rt2_variant_name(lv.value) if lv.value >= 0 else None
-    if not name:
-        return KERNEL_NAMES[traversal]
-    name = name.decode()
-    kern = {"smem": "render_smem", "split": "render_split", "tiled": "render_tiled", "resident": "render_resident",
-            "bvh3": "render_bvh3", "bvh2": "render_bvh2", "bvh": "render_bvh"}
-    for prefix, k in kern.items():
-        if name.startswith(prefix):
-            return f"{k} (rt2_render.hip, variant {name})"
-    return name
+    return name.decode() if name else None
 
 
-def cpu_baseline(sd, spec, u, gpu_image, threads):
-    """Times oracle/ (CPU restatement of compute.glsl) on a strided pixel sample
-    (every k-th pixel in raster order, full spp) and checks the GPU's pixels
-    against it.  Test infrastructure: the oracle is only the checker / baseline
-    here, never the measured path."""
+def kernel_label(variant):
+    if not variant:
+        return None
+    for prefix, k in KERNEL_FILES.items():
+        if variant.startswith(prefix):
+            return f"{k} (rt2_render.hip, variant {variant})"
+    return variant
+
+
+def roofline(tests, visits, kern_ms):
+    """FP32-VALU roofline of one launch: algorithmic FLOP / kernel time."""
+    flops = (FLOP_PER_TEST * tests + FLOP_PER_VISIT * visits) / (kern_ms * 1e-3) / 1e12
+    hbm = BYTES_PER_TEST * tests / (kern_ms * 1e-3) / 1e9
+    return {"bound": "valu", "achieved": round(flops, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(flops / VALU_PEAK_TFLOPS, 4), "traffic": None, "kernel_ms": round(kern_ms, 3),
+            "tests_per_launch": int(tests), "node_visits_per_launch": int(visits),
+            "flop_model": "53 x ray-triangle tests + 24 x BVH interior visits (2 slab boxes)",
+            "hbm_read_algorithmic": {"achieved": round(hbm, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                     "frac": round(hbm / HBM_PEAK_GBS, 3),
+                                     "note": "36 B x tests; >1 = on-chip reuse (effective bandwidth)"}}
+
+
+def attach_traffic(rf, config, variant, kern_ms):
+    """roofline.traffic from profiles/pmc_config<X>.json — only when that PMC
+    profile was taken of this kernel variant built from these kernel sources."""
+    path = os.path.join(ROOT, "profiles", f"pmc_config{config}.json")
+    if not os.path.exists(path):
+        rf["traffic_note"] = f"no PMC profile for config {config}"
+        return
+    with open(path) as f:
+        prof = json.load(f)
+    digest = kernel_source_digest()
+    if prof.get("kernel_variant") != variant or prof.get("kernel_source_sha256") != digest:
+        rf["traffic_note"] = (f"profiles/pmc_config{config}.json was measured on variant "
+                              f"{prof.get('kernel_variant')} / sources {str(prof.get('kernel_source_sha256'))[:12]}, "
+                              f"not this launch ({variant} / {digest[:12]}): traffic not attached")
+        return
+    b = prof.get("hbm_bytes_per_launch")
+    if not b:
+        return
+    rf["traffic"] = b
+    gbs = b / (kern_ms * 1e-3) / 1e9
+    rf["hbm_measured"] = {"achieved": round(gbs, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": round(gbs / HBM_PEAK_GBS, 5),
+                          "source": f"profiles/pmc_config{config}.json (FETCH_SIZE x2 + WRITE_SIZE, separate "
+                                    f"--pmc passes, MI355X_MICROARCH.md HBM section; kernel sources "
+                                    f"{digest[:12]})"}
+
+
+def timed_renders(torch, rt2, scene, u, frames, sh, accum, image, steps, stream):
+    """`steps` renders, each bracketed by HIP events on the stream it runs on;
+    returns (wall seconds, mean kernel ms, stats)."""
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    scene.stats(reset=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        accum.zero_()
+        ev[i][0].record(stream)
+        scene.render(u, 0, frames, sh, accum.data_ptr(), 0, stream.cuda_stream)
+        ev[i][1].record(stream)
+        rt2.resolve_rgba32f(accum.data_ptr(), accum.shape[0] * accum.shape[1], frames, image.data_ptr(),
+                            stream.cuda_stream)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / steps
+    return el, kern_ms, scene.stats(reset=True)
+
+
+def cpu_baseline(sd, spec, u, gpu_images, threads, seconds):
+    """Times oracle/ (CPU restatement of compute.glsl) in both traversals on an
+    evenly spread pixel sample (every k-th pixel in raster order, full spp) of
+    ~`seconds` each, and checks the GPU images' pixels against it (brute GPU
+    image vs brute oracle, BVH vs BVH: bit-exact).  Test infrastructure: the
+    oracle is the checker / baseline here, never the measured path."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle
     tris, mats, nodes = sd.triangles(), sd.materials(), sd.nodes()
     H, W = spec.height, spec.width
     npx_all = H * W
-    res = {}
-    done = {}
+    res, done = {}, {}
     for mode in ("bvh", "brute"):
-        # calibrate on a spread probe, then size the sample to ~cpu_seconds
-        nprobe = 4 * threads
+        nprobe = 2 * threads
         pid = np.linspace(npx_all // 7, npx_all - 1 - npx_all // 7, nprobe).astype(np.int64)
         t0 = time.perf_counter()
         oracle.render_pixels(tris, mats, u, pid % W, pid // W, 0, spec.frames, mode, nodes=nodes, threads=threads)
         dt = max(time.perf_counter() - t0, 1e-3) / nprobe
-        n = int(max(threads, min(npx_all, args.cpu_seconds / dt)))
-        pid = np.arange(n, dtype=np.int64) * npx_all // n  # n pixels spread evenly in raster order
-        xs, ys = pid % W, pid // W
-        t0 = time.perf_counter()
-        acc, _, segs, tests = oracle.render_pixels(tris, mats, u, xs, ys, 0, spec.frames, mode, nodes=nodes,
-                                                   threads=threads)
-        dt = time.perf_counter() - t0
-        if dt < 0.4 * args.cpu_seconds and n < npx_all:  # the probe over-estimated: resize once
-            n = int(min(npx_all, n * args.cpu_seconds / max(dt, 1e-3)))
-            pid = np.arange(n, dtype=np.int64) * npx_all // n
+        n = int(max(threads, min(npx_all, seconds / dt)))
+        for attempt in range(2):
+            pid = np.arange(n, dtype=np.int64) * npx_all // n  # n pixels spread evenly in raster order
             xs, ys = pid % W, pid // W
             t0 = time.perf_counter()
             acc, _, segs, tests = oracle.render_pixels(tris, mats, u, xs, ys, 0, spec.frames, mode, nodes=nodes,
                                                        threads=threads)
             dt = time.perf_counter() - t0
+            if attempt == 1 or dt >= 0.4 * seconds or n >= npx_all:
+                break
+            n = int(min(npx_all, n * seconds / max(dt, 1e-3)))  # the probe over-estimated: resize once
         samples = len(pid) * spec.rays * spec.frames
         res[mode] = dict(value=samples / dt / 1e6, pixels=int(len(pid)), seconds=dt,
                          segments_per_sample=segs / samples, tests_per_segment=tests / max(segs, 1))
         done[mode] = (ys, xs, acc / spec.frames)
+    ds, exact = [], {}
+    for mode, (ys, xs, ref) in done.items():
+        img = gpu_images.get(mode)
+        if img is None:
+            continue
+        d = np.abs(img[ys, xs][..., :3].astype(np.float64) - ref[..., :3])
+        ds.append(d)
+        exact[mode] = float((d.max(-1) == 0).mean())
     parity = None
-    if gpu_image is not None:
-        ds = []
-        fr = {}
-        for mode, (ys, xs, ref) in done.items():
-            d = np.abs(gpu_image[ys, xs][..., :3] - ref[..., :3])
-            ds.append(d)
-            fr[mode] = float((d.max(-1) == 0).mean())
-        parity = dict(pixels=int(sum(len(d) for d in ds)), oracle_modes=list(done),
-                      exact_pixel_frac_brute=fr["brute"], exact_pixel_frac_bvh=fr["bvh"],
-                      rmse=float(np.sqrt(np.concatenate([(d ** 2).ravel() for d in ds]).mean())),
+    if ds:
+        parity = dict(pixels=int(sum(len(d) for d in ds)), pairs="GPU brute vs oracle brute, GPU BVH vs oracle BVH",
+                      exact_pixel_frac=exact, rmse=float(np.sqrt(np.concatenate([(d ** 2).ravel() for d in ds]).mean())),
                       max_abs=float(max(d.max() for d in ds)), tolerance_rmse=1e-4)
     return res, parity
 
 
+def cpu_summary(res, threads, host, sample_desc, gpu_values):
+    """cpu_baseline object: the measured rate on the CPUs this job may use, the
+    host's core counts, and a linear extrapolation to the whole node."""
+    logical, phys = host.get("logical_cpus") or threads, host.get("physical_cores") or threads
+    v = res["bvh"]["value"]
+    node_hi = v / threads * logical   # every hardware thread at the measured per-thread rate (upper bound)
+    node_lo = v / threads * phys      # one thread per physical core (SMT adds nothing)
+    out = {"value": round(v, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+           "sample": sample_desc,
+           "host": {**host, "threads_used": threads,
+                    "note": "threads = the CPUs this job may use: the affinity mask capped by the cgroup CPU quota "
+                            "(a GPU box grants a one-GPU job 16 CPUs of its node; more threads would add no CPU "
+                            "time and exceed the pool's worker sizing)"},
+           "brute_force": {"value": round(res["brute"]["value"], 5), "pixels": res["brute"]["pixels"],
+                           "seconds": round(res["brute"]["seconds"], 2)},
+           "node_extrapolated": {"value_all_logical_cpus": round(node_hi, 3),
+                                 "value_all_physical_cores": round(node_lo, 3),
+                                 "note": "linear scaling of the measured per-thread BVH rate to the node's "
+                                         f"{logical} hardware threads (upper bound) / {phys} physical cores; "
+                                         "an estimate, not a measurement"}}
+    for name, g in gpu_values.items():
+        out[f"gpu_{name}_over_cpu_bvh"] = round(g / v, 2)
+        out[f"gpu_{name}_over_cpu_brute"] = round(g / res["brute"]["value"], 1)
+        out[f"gpu_{name}_over_node_extrapolated_bvh"] = round(g / node_hi, 2)
+    return out
+
+
+def config_c_leg(torch, rt2, stream, threads, host, seconds, do_cpu):
+    """The north-star target configuration on one GPU: brute force (1 timed
+    step: ~1.5 min of kernel) with its roofline, the BVH traversal (3 steps),
+    the CPU baseline on the same sample and parity against the oracle."""
+    import numpy as np
+    sd, spec = rt2.build_config_scene("C")
+    u = rt2.offline_uniforms(spec.width, spec.height, spec.bounces, spec.rays, sd.num_triangles)
+    scene = rt2.Scene(sd, torch.cuda.current_device())
+    sh = rt2.shard()
+    accum = torch.zeros((spec.height, spec.width, 4), dtype=torch.float32, device="cuda")
+    image = torch.empty_like(accum)
+    samples = spec.width * spec.height * spec.rays * spec.frames
+    out = {"workload": f"config C: {spec.description}", "width": spec.width, "height": spec.height,
+           "rays_per_pixel": spec.rays, "frames": spec.frames, "max_bounce": spec.bounces,
+           "triangles": sd.num_triangles}
+    legs, imgs = {}, {}
+    for trav, steps, warm in (("bvh", 3, 1), ("brute", 1, 0)):
+        scene.set_traversal(trav)
+        for _ in range(warm):
+            accum.zero_()
+            scene.render(u, 0, spec.frames, sh, accum.data_ptr(), 0, stream.cuda_stream)
+        el, kern_ms, st = timed_renders(torch, rt2, scene, u, spec.frames, sh, accum, image, steps, stream)
+        variant = launched_variant(rt2, scene)
+        rf = roofline(st.tests / steps, st.node_visits / steps, kern_ms)
+        rf["kernel"] = kernel_label(variant)
+        attach_traffic(rf, "C" if trav == "brute" else "C_bvh", variant, kern_ms)
+        legs[trav] = {"value": round(samples * steps / el / 1e6, 4), "unit": "Msamples/s", "steps": steps,
+                      "ms_per_step": round(el / steps * 1e3, 1), "roofline": rf,
+                      "segments_per_sample": round(st.segments / (samples * steps), 4)}
+        imgs[trav] = image.cpu().numpy()
+    out["brute"], out["bvh"] = legs["brute"], legs["bvh"]
+    nd = int((imgs["brute"][..., :3] != imgs["bvh"][..., :3]).any(-1).sum())
+    out["pixels_brute_vs_bvh_differing"] = nd
+    if do_cpu:
+        res, parity = cpu_baseline(sd, spec, u, imgs, threads, seconds)
+        desc = (f"{res['bvh']['pixels']} of {spec.width * spec.height} pixels (BVH mode; brute mode "
+                f"{res['brute']['pixels']}), evenly spread in raster order, full 256 spp, "
+                f"{res['bvh']['seconds']:.1f} s")
+        cb = cpu_summary(res, threads, host, desc, {"brute": legs["brute"]["value"], "bvh": legs["bvh"]["value"]})
+        out["cpu_baseline"] = cb
+        out["parity"] = parity
+        tgt = {"target": f">= {TARGET_RATIO:g}x the CPU reference's Msamples/s at config C on 1 GPU",
+               "cpu_reference": f"oracle/ BVH traversal (the reference's algorithm) on {threads} CPUs",
+               "brute_ratio": cb["gpu_brute_over_cpu_bvh"], "bvh_ratio": cb["gpu_bvh_over_cpu_bvh"],
+               "met_by_brute": cb["gpu_brute_over_cpu_bvh"] >= TARGET_RATIO,
+               "met_by_bvh": cb["gpu_bvh_over_cpu_bvh"] >= TARGET_RATIO,
+               "bvh_ratio_vs_node_extrapolation": cb["gpu_bvh_over_node_extrapolated_bvh"],
+               "met_by_bvh_vs_node_extrapolation": cb["gpu_bvh_over_node_extrapolated_bvh"] >= TARGET_RATIO}
+        k = [n for n in ("brute", "bvh") if tgt[f"met_by_{n}"]]
+        tgt["statement"] = (f"target met by the {' and '.join(k)} kernel(s)" if k else "target NOT met") + \
+            f" against {threads} CPUs; against all {host.get('logical_cpus')} hardware threads of the node " \
+            f"(extrapolated) the BVH kernel is {cb['gpu_bvh_over_node_extrapolated_bvh']}x"
+        out["north_star_target"] = tgt
+    return out
+
+
 def main():
-    global args
     args = parse()
     import numpy as np
     import torch
@@ -198,7 +363,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     st = scene.stats(reset=True)
-    kernel_name = launched_kernel(rt2, scene, args.traversal)
+    variant = launched_variant(rt2, scene)
     t = torch.tensor([elapsed, kern_ms, float(st.tests), float(st.segments), float(st.node_visits)],
                      dtype=torch.float64, device="cuda")
     if world > 1:
@@ -213,16 +378,17 @@ def main():
 
     samples_per_step = spec.width * spec.height * spec.rays * spec.frames
     value = samples_per_step * args.steps / elapsed / 1e6
-    tests_per_launch = tests / args.steps / world
-    visits_per_launch = visits / args.steps / world
-    flops = (FLOP_PER_TEST * tests_per_launch + FLOP_PER_VISIT * visits_per_launch) / (kern_ms * 1e-3) / 1e12
-    hbm_read = BYTES_PER_TEST * tests_per_launch / (kern_ms * 1e-3) / 1e9
 
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
         return
 
+    rf = roofline(tests / args.steps / world, visits / args.steps / world, kern_ms)
+    rf["kernel"] = kernel_label(variant)
+    rf["segments_per_sample"] = round(segs / (samples_per_step * args.steps), 4)
+    if world == 1:  # PMC traffic was measured for the 1-GPU launch
+        attach_traffic(rf, spec.name if args.traversal == "brute" else f"{spec.name}_bvh", variant, kern_ms)
     out = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -242,29 +408,11 @@ def main():
                    "traversal": "brute force" if args.traversal == "brute" else "BVH (compute.glsl:410-460)",
                    "seed": "x + y*W + frame*968824447", "parallelism": f"row-tile x{world}" if world > 1 else "1 GPU",
                    "tile_rows": args.tile_rows},
-        "roofline": {"bound": "valu", "achieved": round(flops, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(flops / VALU_PEAK_TFLOPS, 4), "traffic": None,
-                     "kernel": kernel_name, "kernel_ms": round(kern_ms, 3),
-                     "tests_per_launch": int(tests_per_launch),
-                     "node_visits_per_launch": int(visits_per_launch),
-                     "flop_model": "53 x ray-triangle tests + 24 x BVH interior visits (2 slab boxes)",
-                     "segments_per_sample": round(segs / (samples_per_step * args.steps), 4),
-                     "hbm_read_algorithmic": {"achieved": round(hbm_read, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                              "frac": round(hbm_read / HBM_PEAK_GBS, 3),
-                                              "note": "36 B x tests; >1 = LDS reuse (effective bandwidth)"}},
+        "roofline": rf,
         "cpu_baseline": None,
     }
-    traffic_file = os.path.join(ROOT, "profiles", f"pmc_config{spec.name}.json")
-    if world == 1 and os.path.exists(traffic_file):  # PMC traffic was measured for the 1-GPU launch
-        with open(traffic_file) as f:
-            out["roofline"]["traffic"] = json.load(f).get("hbm_bytes_per_launch")
-        if out["roofline"]["traffic"]:
-            # rocprof-measured HBM bandwidth of the launch (PMC bytes / this run's kernel time)
-            gbs = out["roofline"]["traffic"] / (kern_ms * 1e-3) / 1e9
-            out["roofline"]["hbm_measured"] = {"achieved": round(gbs, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                               "frac": round(gbs / HBM_PEAK_GBS, 4),
-                                               "source": f"profiles/pmc_config{spec.name}.json (FETCH_SIZE x2 + "
-                                                         f"WRITE_SIZE, MI355X_MICROARCH.md HBM section)"}
+    gpu_imgs = {args.traversal: img.cpu().numpy() if img is not None else None}
+    gpu_values = {args.traversal: value}
     alt = "bvh" if args.traversal == "brute" else "brute"
     # brute force over 100k+ triangles takes minutes per step: not timed beside BVH there
     if world == 1 and not args.no_alt and (alt == "bvh" or sd.num_triangles <= 20000):
@@ -275,54 +423,41 @@ def main():
         scene.set_variant(0)
         renderer.accum.zero_()
         scene.render(u, 0, spec.frames, renderer.sh, renderer.accum.data_ptr(), 0, stream.cuda_stream)
-        torch.cuda.synchronize()
-        scene.stats(reset=True)
-        ev2 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in range(args.steps)]
-        t1 = time.perf_counter()
-        for i in range(args.steps):
-            renderer.accum.zero_()
-            ev2[i][0].record(stream)
-            scene.render(u, 0, spec.frames, renderer.sh, renderer.accum.data_ptr(), 0, stream.cuda_stream)
-            ev2[i][1].record(stream)
-            rt2.resolve_rgba32f(renderer.accum.data_ptr(), renderer.rows * spec.width, spec.frames,
-                                renderer.image.data_ptr(), stream.cuda_stream)
-        torch.cuda.synchronize()
-        el2 = time.perf_counter() - t1
-        st2 = scene.stats(reset=True)
+        el2, km2, st2 = timed_renders(torch, rt2, scene, u, spec.frames, renderer.sh, renderer.accum,
+                                      renderer.image, args.steps, stream)
         ndiff = int((renderer.image[..., :3] != img_main[..., :3]).any(-1).sum().item())
         d2 = (renderer.image[..., :3] - img_main[..., :3]).double()
+        v2 = samples_per_step * args.steps / el2 / 1e6
+        gpu_imgs[alt] = renderer.image.cpu().numpy()
+        gpu_values[alt] = v2
         out["alt_traversal"] = {
-            "traversal": alt, "value": round(samples_per_step * args.steps / el2 / 1e6, 3),
-            "ms_per_step": round(el2 / args.steps * 1e3, 3),
-            "kernel": launched_kernel(rt2, scene, alt),
-            "kernel_ms": round(float(np.mean([a.elapsed_time(b) for a, b in ev2])), 3),
+            "traversal": alt, "value": round(v2, 3), "ms_per_step": round(el2 / args.steps * 1e3, 3),
+            "kernel": kernel_label(launched_variant(rt2, scene)), "kernel_ms": round(km2, 3),
             "segments_per_sample": round(st2.segments / (samples_per_step * args.steps), 4),
             "tests_per_segment": round(st2.tests / max(st2.segments, 1), 3),
             "node_visits_per_segment": round(st2.node_visits / max(st2.segments, 1), 3),
             "valu_tflops": round((FLOP_PER_TEST * st2.tests + FLOP_PER_VISIT * st2.node_visits) / args.steps
-                                 / (float(np.mean([a.elapsed_time(b) for a, b in ev2])) * 1e-3) / 1e12, 3),
+                                 / (km2 * 1e-3) / 1e12, 3),
             "pixels_differing_from_main": ndiff,
             "rmse_vs_main": float(d2.pow(2).mean().sqrt()),
             "note": "brute force and the reference BVH traversal agree except on exact distance ties"}
         scene.set_traversal(args.traversal)
         scene.set_variant(args.variant)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test infrastructure: the CPU baseline and the parity checker only
+    threads, host = oracle.default_threads(), oracle.host_cpu_info()
     if world == 1 and not args.no_cpu_baseline:
-        threads = min(16, os.cpu_count() or 1)
-        gpu_np = img.cpu().numpy() if img is not None else None
-        res, parity = cpu_baseline(sd, spec, u, gpu_np, threads)
-        out["cpu_baseline"] = {"value": round(res["bvh"]["value"], 4), "unit": "Msamples/s", "cores": threads,
-                               "kind": "port",
-                               "sample": f"{res['bvh']['pixels']} of {spec.width * spec.height} pixels, "
-                                         f"i = floor(k*{spec.width * spec.height}/{res['bvh']['pixels']}) in raster "
-                                         f"order, full spp, reference BVH traversal (compute.glsl:410-460), "
-                                         f"{res['bvh']['seconds']:.1f} s",
-                               "brute_force": {"value": round(res["brute"]["value"], 4),
-                                               "pixels": res["brute"]["pixels"],
-                                               "seconds": round(res["brute"]["seconds"], 2)},
-                               "gpu_over_cpu_bvh": round(value / res["bvh"]["value"], 1),
-                               "gpu_over_cpu_brute": round(value / res["brute"]["value"], 1)}
+        res, parity = cpu_baseline(sd, spec, u, gpu_imgs, threads, args.cpu_seconds)
+        desc = (f"{res['bvh']['pixels']} of {spec.width * spec.height} pixels (BVH mode; brute mode "
+                f"{res['brute']['pixels']}), i = floor(k*{spec.width * spec.height}/n) in raster order, full spp, "
+                f"reference BVH traversal (compute.glsl:410-460), {res['bvh']['seconds']:.1f} s")
+        out["cpu_baseline"] = cpu_summary(res, threads, host, desc, gpu_values)
         out["parity"] = parity
+    if world == 1 and spec.name == "B" and not args.no_config_c:
+        scene.close()
+        torch.cuda.empty_cache()
+        out["config_C"] = config_c_leg(torch, rt2, stream, threads, host, args.cpu_seconds,
+                                       not args.no_cpu_baseline)
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

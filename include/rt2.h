@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define RT2_ABI_VERSION 3
+#define RT2_ABI_VERSION 4
 
 /* Material types: mesh.h:16-22 == compute.glsl:7-13 */
 enum {
@@ -184,8 +184,11 @@ int rt2_render(rt2_scene* scene, const rt2_uniforms* uniforms,
                uint32_t frame_begin, uint32_t frame_count, rt2_shard shard,
                float* d_accum, uint32_t* d_accum8, void* stream);
 
-/* Blocking convenience wrapper: renders into internal device buffers and
- * copies the resolved mean image back to host memory.  out_rgba (nullable):
+/* Blocking convenience wrapper — the readback half of screenshot()
+ * (glReadPixels, rayTracing.cpp:217): renders into device buffers the scene
+ * keeps between calls (allocated on first use, freed by rt2_scene_destroy), on
+ * a stream of its own, and copies the resolved mean image back to host memory;
+ * it waits for that stream only.  out_rgba (nullable):
  * rows*W*4 floats, mean over the frames (alpha = 1), slab-row order, slab row
  * 0 = lowest image row (GL convention, row 0 = bottom).  out_rgb8 (nullable):
  * rows*W*3 bytes, the reference's 8-bit screenshot average
@@ -201,6 +204,51 @@ int rt2_resolve_rgba32f(const float* d_accum, int64_t n_pixels, uint32_t frames,
  * u8(min(255, float(sum)/frames)) per channel, rgba sums -> rgb bytes. */
 int rt2_resolve_rgb8_reference(const uint32_t* accum8, int64_t n_pixels, uint32_t frames,
                                uint8_t* out_rgb);
+
+/* ------------------------------------------------------------------------
+ * (1b) Multi-GPU: row-tile shards + one RCCL gather
+ *
+ * The reference renders on one GPU and reads the framebuffer back with
+ * glReadPixels inside screenshot() (rayTracing.cpp:124-283, :217).  With N
+ * ranks (one process per GPU), rank r renders the rows of rt2_shard
+ * {tile_rows, r, N} and ONE ncclGather (RCCL over xGMI) brings the resolved
+ * slabs to the root, which un-interleaves them: bit-identical to one GPU.
+ * ---------------------------------------------------------------------- */
+#define RT2_COMM_ID_BYTES 128 /* sizeof(ncclUniqueId) */
+typedef struct rt2_comm rt2_comm;
+
+/* ncclGetUniqueId: called once (by the root); the bytes travel to the other
+ * ranks by any channel (a file, a socket, an MPI broadcast). */
+int rt2_comm_unique_id(uint8_t* id /* RT2_COMM_ID_BYTES */);
+/* ncclCommInitRank on `device` (blocks until all nranks have joined). */
+int rt2_comm_init(const uint8_t* id, int32_t nranks, int32_t rank, int32_t device, rt2_comm** out);
+/* Uses a caller-owned ncclComm_t (not destroyed by rt2_comm_destroy). */
+int rt2_comm_wrap(void* nccl_comm, int32_t device, rt2_comm** out);
+void rt2_comm_destroy(rt2_comm* comm);
+int rt2_comm_size(rt2_comm* comm, int32_t* nranks, int32_t* rank);
+/* ncclCommGetAsyncError: < 0 (with rt2_last_error) if a collective failed. */
+int rt2_comm_check(rt2_comm* comm);
+
+/* Gathers every rank's slab — rt2_shard_rows(height, shard) rows of `width`
+ * 16-byte pixels (an rgba32f image or the uint32x4 8-bit sums), device memory —
+ * to `root` with one ncclGather and un-interleaves it there into d_image
+ * (height*width pixels, device; ignored on other ranks).  shard.rank/nranks
+ * must be the communicator's.  Asynchronous on `stream`. */
+int rt2_gather_slabs(rt2_comm* comm, const void* d_slab, int32_t width, int32_t height, rt2_shard shard,
+                     int32_t root, void* d_image, void* stream);
+/* The root's un-interleave alone: d_gathered = [nranks][max_rows][width]
+ * 16-byte pixels (rank-major slabs, padded to max_rows rows) -> d_image
+ * [height][width] for the tile layout {tile_rows, -, nranks}.  Async. */
+int rt2_unshard_slabs(const void* d_gathered, int32_t max_rows, int32_t width, int32_t height, rt2_shard layout,
+                      void* d_image, void* stream);
+/* rt2_render_host across ranks: every rank renders its shard, the resolved
+ * slabs (and, if out_rgb8, the 8-bit sums) are gathered to `root`, which
+ * receives the whole image in out_rgba (height*width*4 floats) / out_rgb8
+ * (height*width*3 bytes, not flipped); other ranks' output pointers are
+ * ignored.  Blocking; every rank must call it. */
+int rt2_render_host_gather(rt2_scene* scene, const rt2_uniforms* uniforms, uint32_t frame_begin,
+                           uint32_t frame_count, rt2_shard shard, rt2_comm* comm, int32_t root,
+                           float* out_rgba, uint8_t* out_rgb8);
 
 /* Counters of the renders issued on this scene since the last reset
  * (synchronises the scene's device). */

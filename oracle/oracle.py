@@ -18,6 +18,48 @@ REF_DUMP = os.path.join(HERE, "_ref", "ref_dump")
 _lib = None
 
 
+def cgroup_cpu_quota() -> float | None:
+    """CPUs this process may use per the cgroup v2 CPU controller (cpu.max
+    quota / period), or None when unlimited or unavailable."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        return None
+
+
+def host_cpu_info() -> dict:
+    """The host's CPU as seen from this process: model, logical CPUs, physical
+    cores, the affinity mask and the cgroup CPU quota (a GPU box grants a job a
+    quota far below its core count)."""
+    model, cores_per_socket, sockets = None, None, set()
+    try:
+        for line in open("/proc/cpuinfo"):
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "model name" and model is None:
+                model = v
+            elif k == "cpu cores" and cores_per_socket is None:
+                cores_per_socket = int(v)
+            elif k == "physical id":
+                sockets.add(v)
+    except OSError:
+        pass
+    phys = cores_per_socket * max(len(sockets), 1) if cores_per_socket else None
+    return {"model": model, "logical_cpus": os.cpu_count(), "physical_cores": phys,
+            "affinity_cpus": len(os.sched_getaffinity(0)), "cgroup_cpu_quota": cgroup_cpu_quota()}
+
+
+def default_threads() -> int:
+    """Worker threads for the oracle: every CPU of the affinity mask, capped by
+    the cgroup CPU quota (threads beyond the quota add no CPU time)."""
+    n = len(os.sched_getaffinity(0))
+    q = cgroup_cpu_quota()
+    if q:
+        n = min(n, max(1, int(q + 0.5)))
+    return max(1, n)
+
+
 def build() -> None:
     subprocess.run(["make", "-C", HERE, "liboracle.so"], check=True, stdout=subprocess.DEVNULL)
 
@@ -70,7 +112,7 @@ def render(triangles: np.ndarray, materials: np.ndarray, uniforms, rows, frame_b
     rc = lib().oracle_render(tri.ctypes.data, len(tri), mat.ctypes.data, len(mat),
                              None if nd is None else nd.ctypes.data, 0 if nd is None else len(nd),
                              C.addressof(uniforms), frame_begin, frame_count, rows.ctypes.data, len(rows), m,
-                             threads or os.cpu_count() or 1, acc.ctypes.data,
+                             threads or default_threads(), acc.ctypes.data,
                              None if acc8 is None else acc8.ctypes.data, C.byref(segs), C.byref(tests))
     if rc != 0:
         raise RuntimeError(f"oracle_render failed: {rc}")
@@ -96,7 +138,7 @@ def render_pixels(triangles: np.ndarray, materials: np.ndarray, uniforms, xs, ys
     rc = lib().oracle_render_pixels(tri.ctypes.data, len(tri), mat.ctypes.data, len(mat),
                                     None if nd is None else nd.ctypes.data, 0 if nd is None else len(nd),
                                     C.addressof(uniforms), frame_begin, frame_count, px.ctypes.data, n, m,
-                                    threads or os.cpu_count() or 1, acc.ctypes.data,
+                                    threads or default_threads(), acc.ctypes.data,
                                     None if acc8 is None else acc8.ctypes.data, C.byref(segs), C.byref(tests))
     if rc != 0:
         raise RuntimeError(f"oracle_render_pixels failed: {rc}")

@@ -8,17 +8,25 @@
  *
  *   rt2_screenshot [--model DIR] [--box cornell|mirror|sidelit|sky|classic|diverse|none]
  *                  [--width W] [--height H] [--rays R] [--frames F] [--bounces B]
- *                  [--out PATH] [--float-mean] [--device D]
+ *                  [--out PATH] [--float-mean] [--device D] [--traversal brute|bvh]
+ *                  [--nranks N --rank R --id-file PATH [--tile-rows T]]
  *
  * Default output is the reference's 8-bit path (per-frame unorm8, float sum,
  * truncating average: rayTracing.cpp:217-250); --float-mean writes the
  * mean of the float frames quantised once instead.
+ *
+ * Multi-GPU: start one process per GPU with the same
+ * arguments plus --nranks N --rank R (and --device, default R).  Rank 0 writes
+ * the RCCL communicator id to --id-file, the others read it; every rank
+ * renders the row tiles of rt2_shard {T, R, N}, one RCCL gather brings the
+ * slabs to rank 0, which writes the PNG (identical to a one-GPU run).
  */
-#define _POSIX_C_SOURCE 199309L
+#define _POSIX_C_SOURCE 200809L
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <unistd.h>
 
 #include "../../../include/rt2.h"
 
@@ -33,11 +41,41 @@ static int die(const char* what) {
     return 1;
 }
 
+/* The communicator id travels through a file: rank 0 writes it under a
+ * temporary name and renames it (atomic), the other ranks poll for it. */
+static int exchange_id(const char* path, int rank, uint8_t* id) {
+    if (rank == 0) {
+        if (rt2_comm_unique_id(id)) return die("rt2_comm_unique_id");
+        char tmp[4096];
+        snprintf(tmp, sizeof tmp, "%s.tmp%d", path, (int)getpid());
+        FILE* f = fopen(tmp, "wb");
+        if (!f || fwrite(id, 1, RT2_COMM_ID_BYTES, f) != RT2_COMM_ID_BYTES || fclose(f) != 0 || rename(tmp, path)) {
+            fprintf(stderr, "rt2_screenshot: cannot write %s\n", path);
+            return 1;
+        }
+        return 0;
+    }
+    for (int tries = 0; tries < 6000; tries++) {  /* 60 s */
+        FILE* f = fopen(path, "rb");
+        if (f) {
+            size_t got = fread(id, 1, RT2_COMM_ID_BYTES, f);
+            fclose(f);
+            if (got == RT2_COMM_ID_BYTES) return 0;
+        }
+        struct timespec ts = {0, 10000000};
+        nanosleep(&ts, NULL);
+    }
+    fprintf(stderr, "rt2_screenshot: no communicator id in %s after 60 s\n", path);
+    return 1;
+}
+
 int main(int argc, char** argv) {
     const char* model = NULL;
     const char* box = "cornell";
     const char* out = "test.png";
-    int W = 1000, H = 1000, R = 64, F = 10, B = 20, device = 0, float_mean = 0;
+    const char* id_file = NULL;
+    int W = 1000, H = 1000, R = 64, F = 10, B = 20, device = -1, float_mean = 0;
+    int nranks = 0, rank = 0, tile_rows = 1, bvh = 0;
     for (int i = 1; i < argc; i++) {
         const char* a = argv[i];
         const char* v = i + 1 < argc ? argv[i + 1] : NULL;
@@ -50,12 +88,23 @@ int main(int argc, char** argv) {
         else if (!strcmp(a, "--frames") && v) F = atoi(argv[++i]);
         else if (!strcmp(a, "--bounces") && v) B = atoi(argv[++i]);
         else if (!strcmp(a, "--device") && v) device = atoi(argv[++i]);
+        else if (!strcmp(a, "--nranks") && v) nranks = atoi(argv[++i]);
+        else if (!strcmp(a, "--rank") && v) rank = atoi(argv[++i]);
+        else if (!strcmp(a, "--tile-rows") && v) tile_rows = atoi(argv[++i]);
+        else if (!strcmp(a, "--id-file") && v) id_file = argv[++i];
+        else if (!strcmp(a, "--traversal") && v) bvh = !strcmp(argv[++i], "bvh");
         else if (!strcmp(a, "--float-mean")) float_mean = 1;
         else {
             fprintf(stderr, "unknown argument %s\n", a);
             return 2;
         }
     }
+
+    if (nranks > 0 && (!id_file || rank < 0 || rank >= nranks || tile_rows < 1)) {
+        fprintf(stderr, "rank mode needs --id-file, 0 <= --rank < --nranks and --tile-rows >= 1\n");
+        return 2;
+    }
+    if (device < 0) device = nranks > 0 ? rank : 0;
 
     rt2_scene_data* sd = rt2_sd_create();
     if (!sd) return die("rt2_sd_create");
@@ -102,29 +151,50 @@ int main(int argc, char** argv) {
 
     rt2_uniforms u;
     rt2_uniforms_offline(&u, W, H, B, R, rt2_sd_num_triangles(sd), 0);
+    rt2_comm* comm = NULL;
+    if (nranks > 0) {  /* joins the other ranks (blocks until all have) */
+        uint8_t id[RT2_COMM_ID_BYTES];
+        if (exchange_id(id_file, rank, id)) return 1;
+        if (rt2_comm_init(id, nranks, rank, device, &comm)) return die("rt2_comm_init");
+    }
     rt2_scene* scene = NULL;
     double t0 = now_s();
     if (rt2_scene_create(rt2_sd_triangles(sd), rt2_sd_num_triangles(sd), rt2_sd_materials(sd), rt2_sd_num_materials(sd),
                          rt2_sd_nodes(sd), rt2_sd_num_nodes(sd), device, &scene))
         return die("rt2_scene_create");
+    if (bvh && rt2_scene_set_traversal(scene, RT2_TRAVERSAL_BVH)) return die("traversal");
     double t1 = now_s();
-    rt2_shard all = {1, 0, 1};
     size_t n = (size_t)W * (size_t)H;
     float* rgba = (float*)malloc(n * 16);
     unsigned char* rgb8 = (unsigned char*)malloc(n * 3);
     if (!rgba || !rgb8) return die("malloc");
-    if (rt2_render_host(scene, &u, 0, (uint32_t)F, all, rgba, rgb8)) return die("render");
+    if (nranks > 0) {
+        rt2_shard sh = {tile_rows, rank, nranks};
+        if (rt2_render_host_gather(scene, &u, 0, (uint32_t)F, sh, comm, 0, rgba, rgb8)) return die("render");
+    } else {
+        rt2_shard all = {1, 0, 1};
+        if (rt2_render_host(scene, &u, 0, (uint32_t)F, all, rgba, rgb8)) return die("render");
+    }
     double t2 = now_s();
     rt2_stats st;
     rt2_scene_stats(scene, &st, 1);
     printf("upload %.3f s, render %.3f s, %.2f Msamples/s, %llu segments\n", t1 - t0, t2 - t1,
            (double)st.samples / (t2 - t1) * 1e-6, (unsigned long long)st.segments);
+    if (comm) rt2_comm_destroy(comm);
+    if (rank != 0) {  /* the image lives on rank 0 */
+        free(rgba);
+        free(rgb8);
+        rt2_scene_destroy(scene);
+        rt2_sd_destroy(sd);
+        return 0;
+    }
 
     if (float_mean)
         for (size_t i = 0; i < n; i++)
             for (int c = 0; c < 3; c++) {
                 float v = rgba[4 * i + c] * 255.0f + 0.5f;
-                rgb8[3 * i + c] = (unsigned char)(v > 255.0f ? 255.0f : (v < 0.0f ? 0.0f : v));
+                /* NaN -> 0 (a NaN reaching the unsigned char conversion is undefined) */
+                rgb8[3 * i + c] = (unsigned char)(v > 255.0f ? 255.0f : (v >= 0.0f ? v : 0.0f));
             }
     /* vertical flip, rayTracing.cpp:253-259 */
     for (int y = 0; y < H / 2; y++)

@@ -1,9 +1,31 @@
-// BVH render kernels (calculateRayCollisionBVH, compute.glsl:410-460): v1, v2,
-// v3 (child-pair records, exact Markstein division) and the division check.
+// BVH render kernels (calculateRayCollisionBVH, compute.glsl:410-460): v1
+// (node array, also the traceBasic walk), v2 and v3 (child-pair records, exact
+// Markstein division; v3 is the product kernel) and the division check.
 // Included by rt2_render.hip only (one translation unit; internal linkage).
 #pragma once
 
 namespace {
+
+// Slab-test division of render_bvh3 (all exact: RN32(n/d) bit for bit).
+enum class Slab : int {
+    Markstein = 0,  // two Markstein corrections of RN(n * RN(1/d)) (default)
+    Binary64 = 1,   // RN32(RN64(n * RN64(1/d)))
+    Filtered = 2,   // approximate t, exact slab only on near-ties
+};
+struct Bvh3Spec {
+    int block;
+    int thresh;  // finished lanes of a wave that end its traversal phase
+    Slab slab;
+    int waves;   // minimum waves per SIMD the register allocation must allow (1 = unconstrained)
+    bool diag;   // diagnostic build: occupancy tallies of the traversal loop
+};
+struct Bvh2Spec {
+    int block;
+    int thresh;
+};
+struct BvhSpec {
+    int block;
+};
 
 // ---------------------------------------------------------------------------
 // BVH traversal: calculateRayCollisionBVH, compute.glsl:410-460, per lane.
@@ -81,8 +103,9 @@ __device__ __forceinline__ void closest_bvh(const f3& o, const f3& d, const rt2_
 
 // BVH: per-lane traversal of the reference's node array (nodes uploaded with
 // the scene).  Dynamic LDS = stack_slots * BLOCK ints.
-template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void render_bvh(RenderParams p) {
+template <BvhSpec S>
+__global__ __launch_bounds__(S.block) void render_bvh(RenderParams p) {
+    constexpr int BLOCK = S.block;
     extern __shared__ int bvh_stack[];
     Lane L;
     lane_init(L);
@@ -255,8 +278,9 @@ __device__ __forceinline__ void bvh_step(TravState& T, int* st, const float4* __
     if (T.sp == 0) T.sp = -1;
 }
 
-template <int BLOCK, int THRESH>
-__global__ __launch_bounds__(BLOCK) void render_bvh2(RenderParams p) {
+template <Bvh2Spec S>
+__global__ __launch_bounds__(S.block) void render_bvh2(RenderParams p) {
+    constexpr int BLOCK = S.block, THRESH = S.thresh;
     extern __shared__ int bvh_stack[];
     int* st = bvh_stack + threadIdx.x;
     const float4* __restrict__ recs = p.bvh_recs;
@@ -474,8 +498,10 @@ __device__ __forceinline__ void bvh_leaf3(TravState3& T, int e, const rt2_node* 
     }
 }
 
-template <int BLOCK, int THRESH, int DIV, int WPE, int DIAG = 0>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void render_bvh3(RenderParams p) {
+template <Bvh3Spec S>
+__global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves))) void render_bvh3(RenderParams p) {
+    constexpr int BLOCK = S.block, THRESH = S.thresh, DIV = (int)S.slab;
+    constexpr bool DIAG = S.diag;
     extern __shared__ int bvh_stack[];
     int* st = bvh_stack + threadIdx.x;
     const float4* __restrict__ recs = p.bvh_recs;

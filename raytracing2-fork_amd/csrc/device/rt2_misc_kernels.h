@@ -285,6 +285,18 @@ __global__ void resolve_kernel(const float4* acc, long long n, float inv_frames_
     out[i] = make_float4(a.x / frames, a.y / frames, a.z / frames, 1.0f);
 }
 
+// The reference screenshot's 8-bit average (rayTracing.cpp:248-250) on the
+// device: u8(min(255, float(sum) / frames)) per channel, rgba sums -> rgb
+// bytes; the same operations as the host rt2_resolve_rgb8_reference.
+__global__ void resolve_rgb8_kernel(const uint4* acc8, long long n, float frames, uint8_t* out) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint4 q = acc8[i];
+    out[3 * i + 0] = (uint8_t)fminf(255.0f, (float)q.x / frames);
+    out[3 * i + 1] = (uint8_t)fminf(255.0f, (float)q.y / frames);
+    out[3 * i + 2] = (uint8_t)fminf(255.0f, (float)q.z / frames);
+}
+
 // Numerics self-test: the IEEE primitives and pinned functions the path uses,
 // evaluated on the device for comparison with the host (tests/test_gpu_numerics.py).
 __global__ void selftest_kernel(const float* in, int n, float* out) {

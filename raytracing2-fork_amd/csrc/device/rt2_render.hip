@@ -96,6 +96,14 @@ struct rt2_scene {
     unsigned long long diag[kCounters] = {};
     int num_cus = 256;
     size_t max_lds = 65536;
+    // rt2_render_host: device buffers reused across calls (grown on demand,
+    // freed with the scene) and the stream the blocking wrapper runs on
+    hipStream_t host_stream = nullptr;
+    float4* d_host_acc = nullptr;   // float accumulator
+    float4* d_host_res = nullptr;   // resolved mean
+    uint4* d_host_acc8 = nullptr;   // 8-bit path sums
+    uint8_t* d_host_rgb8 = nullptr; // 8-bit path result (3 B per pixel)
+    size_t host_cap = 0;            // pixels the four buffers hold
 };
 
 // Validates a reference node array (BVH.h layout) against the triangle count
@@ -363,6 +371,7 @@ static int scene_init(rt2_scene* s, const rt2_triangle* tris, int32_t n_tris, co
         hipLaunchKernelGGL(prep_triangles, dim3((n_tris + 255) / 256), dim3(256), 0, 0, s->d_raw, n_tris, s->d_tri,
                            s->d_mtl);
         HIPCHECK(hipGetLastError());
+#ifdef RT2_EXPERIMENTS
         HIPCHECK(hipMalloc(&s->d_plk, nt * 4 * sizeof(float4)));
         // two scratch words in an unused counter slot (zeroed again below)
         uint32_t* d_flags = reinterpret_cast<uint32_t*>(s->d_counters + kCounters - 2);
@@ -375,6 +384,7 @@ static int scene_init(rt2_scene* s, const rt2_triangle* tris, int32_t n_tris, co
         s->plk_outside = (int)flags[0];
         s->plk_ok = (unsigned long long)flags[0] * 64 <= (unsigned long long)n_tris;  // <= 1/64 always-pass records
         std::memcpy(&s->plk_A, &flags[1], sizeof(float));
+#endif
     }
     HIPCHECK(hipDeviceSynchronize());
     return 0;
@@ -398,6 +408,11 @@ extern "C" void rt2_scene_destroy(rt2_scene* s) {
     (void)hipFree(s->d_texels);
     (void)hipFree(s->d_tex_desc);
     (void)hipFree(s->d_counters);
+    (void)hipFree(s->d_host_acc);
+    (void)hipFree(s->d_host_res);
+    (void)hipFree(s->d_host_acc8);
+    (void)hipFree(s->d_host_rgb8);
+    if (s->host_stream) (void)hipStreamDestroy(s->host_stream);
     delete s;
 }
 
@@ -414,180 +429,147 @@ extern "C" int32_t rt2_shard_row(int32_t local_row, rt2_shard sh) {
     return (t * sh.nranks + sh.rank) * sh.tile_rows + local_row % sh.tile_rows;
 }
 
-extern "C" int rt2_scene_set_variant(rt2_scene* s, int variant) {
-    if (!s) return -1;
-    s->variant = variant;
-    return variant;
-}
 
 namespace {
 constexpr int kTileTris = 1024;  // 48 KiB of LDS per tile
 
-// Kernel variants (rt2_scene_set_variant); 0 = auto = the default below.
+// Kernel variants (rt2_scene_set_variant).  Ids are stable across builds: the
+// product build carries the variants the launcher chooses automatically; the
+// A/B experiments measured in DESIGN.md ("Tried and measured") are compiled
+// only with -DRT2_EXPERIMENTS (make EXPERIMENTS=1).
 enum Kind : int { K_RESIDENT = 0, K_TILED = 1, K_SMEM = 2, K_SPLIT = 3, K_BVH = 4, K_BVH2 = 5, K_BVH3 = 6 };
 struct Variant {
+    int id;
     int kind;
     int block;
     hipError_t (*launch)(const RenderParams&, int blocks, size_t lds, hipStream_t st);
-    hipError_t (*occupancy)(int* occ, size_t lds);
-    const void* (*kernel)();
+    const void* kernel;
     const char* name;
 };
 
-template <int KIND, int BLOCK, int MT, int UNROLL>
-hipError_t launch_t(const RenderParams& p, int blocks, size_t lds, hipStream_t st) {
-    if constexpr (KIND == K_TILED)
-        hipLaunchKernelGGL((render_tiled<BLOCK, MT, UNROLL>), dim3(blocks), dim3(BLOCK), lds, st, p);
-    else if constexpr (KIND == K_SMEM)
-        hipLaunchKernelGGL((render_smem<BLOCK, MT % 1000, MT / 1000, UNROLL>), dim3(blocks), dim3(BLOCK), 0, st, p);
-    else if constexpr (KIND == K_SPLIT)
-        hipLaunchKernelGGL((render_split<BLOCK / 64, MT % 1000, MT / 1000, UNROLL>), dim3(blocks), dim3(BLOCK), 0, st,
-                           p);
-    else if constexpr (KIND == K_BVH)
-        hipLaunchKernelGGL((render_bvh<BLOCK>), dim3(blocks), dim3(BLOCK), lds, st, p);
-    else if constexpr (KIND == K_BVH2)
-        hipLaunchKernelGGL((render_bvh2<BLOCK, MT>), dim3(blocks), dim3(BLOCK), lds, st, p);
-    else if constexpr (KIND == K_BVH3)
-        hipLaunchKernelGGL((render_bvh3<BLOCK, MT % 1000, (MT / 1000) % 10, UNROLL, MT / 10000>), dim3(blocks),
-                           dim3(BLOCK), lds, st, p);
-    else
-        hipLaunchKernelGGL((render_resident<BLOCK, MT, UNROLL>), dim3(blocks), dim3(BLOCK), lds, st, p);
+template <auto K, int BLOCK>
+hipError_t launch_k(const RenderParams& p, int blocks, size_t lds, hipStream_t st) {
+    hipLaunchKernelGGL(K, dim3(blocks), dim3(BLOCK), lds, st, p);
     return hipGetLastError();
 }
-template <int KIND, int BLOCK, int MT, int UNROLL>
-const void* kptr_t() {
-    if constexpr (KIND == K_TILED)
-        return reinterpret_cast<const void*>(render_tiled<BLOCK, MT, UNROLL>);
-    else if constexpr (KIND == K_SMEM)
-        return reinterpret_cast<const void*>(render_smem<BLOCK, MT % 1000, MT / 1000, UNROLL>);
-    else if constexpr (KIND == K_SPLIT)
-        return reinterpret_cast<const void*>(render_split<BLOCK / 64, MT % 1000, MT / 1000, UNROLL>);
-    else if constexpr (KIND == K_BVH)
-        return reinterpret_cast<const void*>(render_bvh<BLOCK>);
-    else if constexpr (KIND == K_BVH2)
-        return reinterpret_cast<const void*>(render_bvh2<BLOCK, MT>);
-    else if constexpr (KIND == K_BVH3)
-        return reinterpret_cast<const void*>(render_bvh3<BLOCK, MT % 1000, (MT / 1000) % 10, UNROLL, MT / 10000>);
-    else
-        return reinterpret_cast<const void*>(render_resident<BLOCK, MT, UNROLL>);
+#define RT2_VARIANT(ID, KIND, KERNEL, BLOCK, NAME) \
+    Variant { ID, KIND, BLOCK, launch_k<KERNEL, BLOCK>, reinterpret_cast<const void*>(KERNEL), NAME }
+
+// product kernels
+constexpr SmemSpec kSmemDefault{.block = 256, .group = 8, .filter = Filter::Max3, .tail = Tail::Coop,
+                                .tail_lanes = 32, .waves = 6, .stats = false};
+constexpr SmemSpec kSmemMid{.block = 256, .group = 8, .filter = Filter::Max3, .tail = Tail::Coop, .tail_lanes = 32,
+                            .waves = 1, .stats = false};
+constexpr SplitSpec kSplitSmall{.waves_per_ray = 4, .group = 8, .filter = Filter::Max3, .waves = 6};
+constexpr TiledSpec kTiledLarge{.block = 512, .group = 4, .filter = Filter::Max3};
+constexpr Bvh3Spec kBvhDefault{.block = 256, .thresh = 16, .slab = Slab::Markstein, .waves = 5, .diag = false};
+
+#ifdef RT2_EXPERIMENTS
+constexpr SmemSpec smem_x(int g, Filter f, Tail t, int lanes, int w, bool stats = false) {
+    return SmemSpec{.block = 256, .group = g, .filter = f, .tail = t, .tail_lanes = lanes, .waves = w, .stats = stats};
 }
-template <int KIND, int BLOCK, int MT, int UNROLL>
-hipError_t occ_t(int* occ, size_t lds) {
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, kptr_t<KIND, BLOCK, MT, UNROLL>(), BLOCK, lds);
+constexpr SplitSpec split_x(int s, Filter f, int w) {
+    return SplitSpec{.waves_per_ray = s, .group = 8, .filter = f, .waves = w};
 }
-#define RT2_VARIANT(T, B, M, U, NAME) Variant{T, B, launch_t<T, B, M, U>, occ_t<T, B, M, U>, kptr_t<T, B, M, U>, NAME}
+constexpr Bvh3Spec bvh3_x(int t, Slab sl, int w, bool diag = false) {
+    return Bvh3Spec{.block = 256, .thresh = t, .slab = sl, .waves = w, .diag = diag};
+}
+#endif
 
 const Variant kVariants[] = {
-    RT2_VARIANT(K_SMEM, 256, 32508, 6, "smem/256/max3f8/coop32/w6"), // 0: default (<= kSmemMaxTris)
-    RT2_VARIANT(K_RESIDENT, 256, 0, 4, "resident/256/plain/u4"),     // 1: round-1 v1 kernel
-    RT2_VARIANT(K_TILED, 512, 4, 1, "tiled/512/grouped4"),           // 2: round-1 large-scene default
-    RT2_VARIANT(K_RESIDENT, 256, 1, 4, "resident/256/filtered/u4"),  // 3
-    RT2_VARIANT(K_RESIDENT, 1024, 1, 4, "resident/1024/filtered/u4"),// 4
-    RT2_VARIANT(K_RESIDENT, 512, 1, 4, "resident/512/filtered/u4"),  // 5
-    RT2_VARIANT(K_RESIDENT, 512, 1, 8, "resident/512/filtered/u8"),  // 6
-    RT2_VARIANT(K_TILED, 256, 1, 4, "tiled/256/filtered/u4"),        // 7
-    RT2_VARIANT(K_TILED, 1024, 4, 1, "tiled/1024/grouped4"),         // 8
-    RT2_VARIANT(K_RESIDENT, 512, 4, 1, "resident/512/grouped4"),     // 9
-    RT2_VARIANT(K_RESIDENT, 1024, 8, 1, "resident/1024/grouped8"),   // 10
-    RT2_VARIANT(K_RESIDENT, 1024, 4, 1, "resident/1024/grouped4"),   // 11
-    RT2_VARIANT(K_RESIDENT, 256, 4, 1, "resident/256/grouped4"),     // 12
-    RT2_VARIANT(K_TILED, 512, 8, 1, "tiled/512/grouped8"),           // 13
-    RT2_VARIANT(K_RESIDENT, 512, 2, 1, "resident/512/grouped2"),     // 14
-    RT2_VARIANT(K_RESIDENT, 512, 4, 0, "resident/512/grouped4/STATS"), // 15: diagnostic counters
-    RT2_VARIANT(K_SMEM, 256, 4, 1, "smem/256/grouped4"),             // 16
-    RT2_VARIANT(K_SMEM, 512, 4, 1, "smem/512/grouped4"),             // 17
-    RT2_VARIANT(K_SMEM, 1024, 4, 1, "smem/1024/grouped4"),           // 18
-    RT2_VARIANT(K_SMEM, 512, 2, 1, "smem/512/grouped2"),             // 19
-    RT2_VARIANT(K_SMEM, 512, 8, 1, "smem/512/grouped8"),             // 20
-    RT2_VARIANT(K_RESIDENT, 512, 104, 1, "resident/512/masked4"),    // 21
-    RT2_VARIANT(K_RESIDENT, 512, 108, 1, "resident/512/masked8"),    // 22
-    RT2_VARIANT(K_SMEM, 256, 104, 1, "smem/256/masked4"),            // 23
-    RT2_VARIANT(K_SMEM, 256, 108, 1, "smem/256/masked8"),            // 24
-    RT2_VARIANT(K_SMEM, 512, 104, 1, "smem/512/masked4"),            // 25
-    RT2_VARIANT(K_TILED, 512, 104, 1, "tiled/512/masked4"),          // 26
-    RT2_VARIANT(K_SMEM, 256, 16108, 1, "smem/256/masked8/coop16"),   // 27
-    RT2_VARIANT(K_SMEM, 256, 32108, 1, "smem/256/masked8/coop32"),   // 28
-    RT2_VARIANT(K_SMEM, 256, 48108, 1, "smem/256/masked8/coop48"),   // 29
-    RT2_VARIANT(K_SMEM, 256, 64108, 1, "smem/256/masked8/coop64"),   // 30
-    RT2_VARIANT(K_SMEM, 256, 208, 1, "smem/256/lean8"),              // 31
-    RT2_VARIANT(K_SMEM, 256, 204, 1, "smem/256/lean4"),              // 32
-    RT2_VARIANT(K_RESIDENT, 1024, 208, 1, "resident/1024/lean8"),    // 33
-    RT2_VARIANT(K_RESIDENT, 1024, 204, 1, "resident/1024/lean4"),    // 34
-    RT2_VARIANT(K_RESIDENT, 512, 208, 1, "resident/512/lean8"),      // 35
-    RT2_VARIANT(K_SMEM, 512, 208, 1, "smem/512/lean8"),              // 36
-    RT2_VARIANT(K_BVH, 256, 0, 1, "bvh/256"),                        // 37: default (BVH traversal)
-    RT2_VARIANT(K_BVH, 128, 0, 1, "bvh/128"),                        // 38
-    RT2_VARIANT(K_BVH, 512, 0, 1, "bvh/512"),                        // 39
-    RT2_VARIANT(K_BVH2, 256, 16, 1, "bvh2/256/t16"),                 // 40
-    RT2_VARIANT(K_BVH2, 256, 8, 1, "bvh2/256/t8"),                   // 41
-    RT2_VARIANT(K_BVH2, 256, 32, 1, "bvh2/256/t32"),                 // 42
-    RT2_VARIANT(K_BVH2, 128, 16, 1, "bvh2/128/t16"),                 // 43
-    RT2_VARIANT(K_BVH2, 64, 16, 1, "bvh2/64/t16"),                   // 44
-    RT2_VARIANT(K_BVH2, 256, 1, 1, "bvh2/256/t1"),                   // 45
-    RT2_VARIANT(K_BVH3, 256, 16, 1, "bvh3/256/t16"),                 // 46
-    RT2_VARIANT(K_BVH3, 256, 8, 1, "bvh3/256/t8"),                   // 47
-    RT2_VARIANT(K_BVH3, 256, 24, 1, "bvh3/256/t24"),                 // 48
-    RT2_VARIANT(K_BVH3, 128, 16, 1, "bvh3/128/t16"),                 // 49
-    RT2_VARIANT(K_BVH3, 256, 1016, 1, "bvh3/256/t16/div64"),         // 50
-    RT2_VARIANT(K_BVH3, 256, 1008, 1, "bvh3/256/t8/div64"),          // 51
-    RT2_VARIANT(K_SMEM, 256, 32108, 6, "smem/256/masked8/coop32/w6"), // 52
-    RT2_VARIANT(K_BVH3, 256, 16, 5, "bvh3/256/t16/w5"),              // 53
-    RT2_VARIANT(K_BVH3, 256, 8, 5, "bvh3/256/t8/w5"),                // 54
-    RT2_VARIANT(K_BVH3, 256, 2016, 5, "bvh3/256/t16/filt/w5"),       // 55
-    RT2_VARIANT(K_BVH3, 256, 2008, 5, "bvh3/256/t8/filt/w5"),        // 56
-    RT2_VARIANT(K_BVH3, 256, 2016, 1, "bvh3/256/t16/filt"),          // 57
-    RT2_VARIANT(K_BVH3, 256, 10016, 5, "bvh3/256/t16/w5/DIAG"),      // 58: diagnostic counters
-    RT2_VARIANT(K_SMEM, 256, 32308, 1, "smem/256/ballot8/coop32"),   // 59
-    RT2_VARIANT(K_SMEM, 256, 32408, 1, "smem/256/minfilt8/coop32"),  // 60
-    RT2_VARIANT(K_SMEM, 256, 32304, 1, "smem/256/ballot4/coop32"),   // 61
-    RT2_VARIANT(K_SMEM, 256, 32416, 1, "smem/256/minfilt16/coop32"), // 62
-    RT2_VARIANT(K_SMEM, 256, 32404, 1, "smem/256/minfilt4/coop32"),  // 63
-    RT2_VARIANT(K_SMEM, 256, 132108, 1, "smem/256/masked8/team32"),  // 64
-    RT2_VARIANT(K_SMEM, 256, 148108, 1, "smem/256/masked8/team48"),  // 65
-    RT2_VARIANT(K_SMEM, 256, 164108, 1, "smem/256/masked8/team64"),  // 66
-    RT2_VARIANT(K_SMEM, 256, 32508, 1, "smem/256/max3f8/coop32"),    // 67
-    RT2_VARIANT(K_SMEM, 256, 32504, 1, "smem/256/max3f4/coop32"),    // 68
-    RT2_VARIANT(K_SMEM, 256, 32508, 6, "smem/256/max3f8/coop32/w6"), // 69
-    RT2_VARIANT(K_SPLIT, 128, 8, 5, "split2/masked8/w5"),            // 70
-    RT2_VARIANT(K_SPLIT, 256, 8, 5, "split4/masked8/w5"),            // 71
-    RT2_VARIANT(K_SPLIT, 128, 1008, 5, "split2/max3f8/w5"),          // 72
-    RT2_VARIANT(K_SPLIT, 256, 1008, 5, "split4/max3f8/w5"),          // 73
-    RT2_VARIANT(K_SMEM, 256, 32604, 1, "smem/256/plk4/coop32"),      // 74
-    RT2_VARIANT(K_SMEM, 256, 32606, 1, "smem/256/plk6/coop32"),      // 75
-    RT2_VARIANT(K_SMEM, 256, 32608, 1, "smem/256/plk8/coop32"),      // 76
-    RT2_VARIANT(K_SMEM, 256, 32604, 6, "smem/256/plk4/coop32/w6"),   // 77
-    RT2_VARIANT(K_SMEM, 256, 32606, 6, "smem/256/plk6/coop32/w6"),   // 78
-    RT2_VARIANT(K_SMEM, 256, 32608, 6, "smem/256/plk8/coop32/w6"),   // 79
-    RT2_VARIANT(K_SMEM, 256, 32602, 1, "smem/256/plk2/coop32"),      // 80
-    RT2_VARIANT(K_SMEM, 256, 32704, 1, "smem/256/plk4/coop32/STATS"), // 81: diagnostic counters
-    RT2_VARIANT(K_SMEM, 256, 32808, 1, "smem/256/max3f8/coop32/STATS"), // 82: diagnostic counters
-    RT2_VARIANT(K_SPLIT, 512, 8, 4, "split8/masked8/w4"),            // 83
-    RT2_VARIANT(K_SPLIT, 512, 1008, 4, "split8/max3f8/w4"),          // 84
-    RT2_VARIANT(K_SPLIT, 256, 1008, 6, "split4/max3f8/w6"),          // 85
-    RT2_VARIANT(K_TILED, 512, 504, 1, "tiled/512/max3f4"),           // 86: default (large scenes)
-    RT2_VARIANT(K_TILED, 512, 508, 1, "tiled/512/max3f8"),           // 87
-    RT2_VARIANT(K_TILED, 256, 508, 1, "tiled/256/max3f8"),           // 88
-    RT2_VARIANT(K_TILED, 1024, 504, 1, "tiled/1024/max3f4"),         // 89
+    RT2_VARIANT(0, K_SMEM, render_smem<kSmemDefault>, 256, "smem/256/max3f8/coop32/w6"),  // default (<= kSmemMaxTris)
+    RT2_VARIANT(53, K_BVH3, render_bvh3<kBvhDefault>, 256, "bvh3/256/t16/w5"),            // default (BVH traversal)
+    RT2_VARIANT(67, K_SMEM, render_smem<kSmemMid>, 256, "smem/256/max3f8/coop32"),         // 1-4 items per lane
+    RT2_VARIANT(85, K_SPLIT, render_split<kSplitSmall>, 256, "split4/max3f8/w6"),          // < 1 item per lane
+    RT2_VARIANT(86, K_TILED, render_tiled<kTiledLarge>, 512, "tiled/512/max3f4"),          // > kSmemMaxTris
+#ifdef RT2_EXPERIMENTS
+    RT2_VARIANT(22, K_RESIDENT, (render_resident<ResidentSpec{512, 8, Filter::Five}>), 512, "resident/512/masked8"),
+    RT2_VARIANT(24, K_SMEM, render_smem<smem_x(8, Filter::Five, Tail::None, 0, 1)>, 256, "smem/256/masked8"),
+    RT2_VARIANT(26, K_TILED, (render_tiled<TiledSpec{512, 4, Filter::Five}>), 512, "tiled/512/masked4"),
+    RT2_VARIANT(27, K_SMEM, render_smem<smem_x(8, Filter::Five, Tail::Coop, 16, 1)>, 256, "smem/256/masked8/coop16"),
+    RT2_VARIANT(28, K_SMEM, render_smem<smem_x(8, Filter::Five, Tail::Coop, 32, 1)>, 256, "smem/256/masked8/coop32"),
+    RT2_VARIANT(29, K_SMEM, render_smem<smem_x(8, Filter::Five, Tail::Coop, 48, 1)>, 256, "smem/256/masked8/coop48"),
+    RT2_VARIANT(30, K_SMEM, render_smem<smem_x(8, Filter::Five, Tail::Coop, 64, 1)>, 256, "smem/256/masked8/coop64"),
+    RT2_VARIANT(37, K_BVH, render_bvh<BvhSpec{256}>, 256, "bvh/256"),
+    RT2_VARIANT(40, K_BVH2, (render_bvh2<Bvh2Spec{256, 16}>), 256, "bvh2/256/t16"),
+    RT2_VARIANT(41, K_BVH2, (render_bvh2<Bvh2Spec{256, 8}>), 256, "bvh2/256/t8"),
+    RT2_VARIANT(43, K_BVH2, (render_bvh2<Bvh2Spec{128, 16}>), 128, "bvh2/128/t16"),
+    RT2_VARIANT(45, K_BVH2, (render_bvh2<Bvh2Spec{256, 1}>), 256, "bvh2/256/t1"),
+    RT2_VARIANT(46, K_BVH3, render_bvh3<bvh3_x(16, Slab::Markstein, 1)>, 256, "bvh3/256/t16"),
+    RT2_VARIANT(47, K_BVH3, render_bvh3<bvh3_x(8, Slab::Markstein, 1)>, 256, "bvh3/256/t8"),
+    RT2_VARIANT(48, K_BVH3, render_bvh3<bvh3_x(24, Slab::Markstein, 1)>, 256, "bvh3/256/t24"),
+    RT2_VARIANT(50, K_BVH3, render_bvh3<bvh3_x(16, Slab::Binary64, 1)>, 256, "bvh3/256/t16/div64"),
+    RT2_VARIANT(52, K_SMEM, render_smem<smem_x(8, Filter::Five, Tail::Coop, 32, 6)>, 256, "smem/256/masked8/coop32/w6"),
+    RT2_VARIANT(54, K_BVH3, render_bvh3<bvh3_x(8, Slab::Markstein, 5)>, 256, "bvh3/256/t8/w5"),
+    RT2_VARIANT(55, K_BVH3, render_bvh3<bvh3_x(16, Slab::Filtered, 5)>, 256, "bvh3/256/t16/filt/w5"),
+    RT2_VARIANT(58, K_BVH3, render_bvh3<bvh3_x(16, Slab::Markstein, 5, true)>, 256, "bvh3/256/t16/w5/DIAG"),
+    RT2_VARIANT(64, K_SMEM, render_smem<smem_x(8, Filter::Five, Tail::Team, 32, 1)>, 256, "smem/256/masked8/team32"),
+    RT2_VARIANT(65, K_SMEM, render_smem<smem_x(8, Filter::Five, Tail::Team, 48, 1)>, 256, "smem/256/masked8/team48"),
+    RT2_VARIANT(66, K_SMEM, render_smem<smem_x(8, Filter::Five, Tail::Team, 64, 1)>, 256, "smem/256/masked8/team64"),
+    RT2_VARIANT(68, K_SMEM, render_smem<smem_x(4, Filter::Max3, Tail::Coop, 32, 1)>, 256, "smem/256/max3f4/coop32"),
+    RT2_VARIANT(70, K_SPLIT, render_split<split_x(2, Filter::Five, 5)>, 128, "split2/masked8/w5"),
+    RT2_VARIANT(71, K_SPLIT, render_split<split_x(4, Filter::Five, 5)>, 256, "split4/masked8/w5"),
+    RT2_VARIANT(72, K_SPLIT, render_split<split_x(2, Filter::Max3, 5)>, 128, "split2/max3f8/w5"),
+    RT2_VARIANT(73, K_SPLIT, render_split<split_x(4, Filter::Max3, 5)>, 256, "split4/max3f8/w5"),
+    RT2_VARIANT(74, K_SMEM, render_smem<smem_x(4, Filter::Plk, Tail::Coop, 32, 1)>, 256, "smem/256/plk4/coop32"),
+    RT2_VARIANT(76, K_SMEM, render_smem<smem_x(8, Filter::Plk, Tail::Coop, 32, 1)>, 256, "smem/256/plk8/coop32"),
+    RT2_VARIANT(79, K_SMEM, render_smem<smem_x(8, Filter::Plk, Tail::Coop, 32, 6)>, 256, "smem/256/plk8/coop32/w6"),
+    RT2_VARIANT(80, K_SMEM, render_smem<smem_x(2, Filter::Plk, Tail::Coop, 32, 1)>, 256, "smem/256/plk2/coop32"),
+    RT2_VARIANT(81, K_SMEM, render_smem<smem_x(4, Filter::Plk, Tail::Coop, 32, 1, true)>, 256,
+                "smem/256/plk4/coop32/STATS"),
+    RT2_VARIANT(82, K_SMEM, render_smem<smem_x(8, Filter::Max3, Tail::Coop, 32, 1, true)>, 256,
+                "smem/256/max3f8/coop32/STATS"),
+    RT2_VARIANT(84, K_SPLIT, render_split<split_x(8, Filter::Max3, 4)>, 512, "split8/max3f8/w4"),
+    RT2_VARIANT(87, K_TILED, (render_tiled<TiledSpec{512, 8, Filter::Max3}>), 512, "tiled/512/max3f8"),
+    RT2_VARIANT(89, K_TILED, (render_tiled<TiledSpec{1024, 4, Filter::Max3}>), 1024, "tiled/1024/max3f4"),
+#endif
 };
-constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr size_t kResidentMaxBytes = 112 * 1024;
 constexpr int kSmemMaxTris = 131072;  // scalar path up to 6.3 MB of records (config C: 781 vs 817 ms tiled; config E: tiled 1,704 vs 2,312 ms)
-constexpr int kDefaultBvhVariant = 53;
-constexpr int kSmallSlabVariant = 85;  // split4/max3f8/w6: brute force on slabs with fewer items than lanes
-constexpr int kLargeSceneVariant = 86;  // tiled/512/max3f4: LDS tiles above kSmemMaxTris triangles
-constexpr int kMidSlabVariant = 67;    // smem/256/max3f8/coop32 (5 waves/SIMD): 1 to 4 items per lane
+constexpr int kDefaultBrute = 0;
+constexpr int kDefaultBvh = 53;
+constexpr int kSmallSlab = 85;   // split4/max3f8/w6: brute force on slabs with fewer items than lanes
+constexpr int kLargeScene = 86;  // tiled/512/max3f4: LDS tiles above kSmemMaxTris triangles
+constexpr int kMidSlab = 67;     // smem/256/max3f8/coop32 (5 waves/SIMD): 1 to 4 items per lane
+
+const Variant* find_variant(int id) {
+    for (const Variant& v : kVariants)
+        if (v.id == id) return &v;
+    return nullptr;
+}
+hipError_t variant_occupancy(const Variant& v, int* occ, size_t lds) {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, v.kernel, v.block, lds);
+}
 }  // namespace
 
-extern "C" const char* rt2_variant_name(int v) { return v >= 0 && v < kNumVariants ? kVariants[v].name : nullptr; }
+extern "C" int rt2_scene_set_variant(rt2_scene* s, int variant) {
+    if (!s) {
+        rt2h::set_error("rt2_scene_set_variant: null scene");
+        return -1;
+    }
+    if (variant != 0 && !find_variant(variant)) {
+        rt2h::set_error("rt2_scene_set_variant: variant " + std::to_string(variant) +
+                        " is not in this build (experiment variants need make EXPERIMENTS=1)");
+        return -1;
+    }
+    s->variant = variant;
+    return variant;
+}
+
+extern "C" const char* rt2_variant_name(int v) {
+    const Variant* V = find_variant(v);
+    return V ? V->name : nullptr;
+}
 
 // Not in rt2.h (diagnostics): the occupancy API's blocks per CU and the
 // kernel's register counts (hipFuncGetAttributes) for variant v.
 extern "C" int rt2_variant_occupancy(int v, int* api_blocks, int* num_regs, int* local_bytes) {
-    if (v < 0 || v >= kNumVariants) return -1;
+    const Variant* V = find_variant(v);
+    if (!V) return -1;
     int occ = 0;
-    HIPCHECK(kVariants[v].occupancy(&occ, 0));
+    HIPCHECK(variant_occupancy(*V, &occ, 0));
     hipFuncAttributes a;
-    HIPCHECK(hipFuncGetAttributes(&a, kVariants[v].kernel()));
+    HIPCHECK(hipFuncGetAttributes(&a, V->kernel));
     if (api_blocks) *api_blocks = occ;
     if (num_regs) *num_regs = a.numRegs;
     if (local_bytes) *local_bytes = (int)a.localSizeBytes;
@@ -759,41 +741,42 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     }
     const size_t resident_bytes = (size_t)3 * sizeof(float4) * (size_t)std::max(s->n_tris, 1);
     const bool fits = resident_bytes <= kResidentMaxBytes;
-    int vi = s->variant;
-    // auto: scalar-path kernel for small scenes (config B: 1,208 triangles),
-    // LDS-tiled sweep for large ones (config C/E: 100k-1M triangles)
-    if (s->traversal == RT2_TRAVERSAL_BVH) {
-        if (vi <= 0 || vi >= kNumVariants || kVariants[vi].kind < K_BVH)
-            vi = kDefaultBvhVariant;
-    } else {
-        if (vi <= 0 || vi >= kNumVariants || kVariants[vi].kind >= K_BVH) {
-            vi = s->n_tris <= kSmemMaxTris ? 0 : kLargeSceneVariant;
-            if (vi == 0) {
-                // items per resident lane decide the tail: a lane ends on a
-                // whole item, so with few items per lane the last round runs
-                // partly empty.  >= 4 per lane at 6 waves/SIMD (a full config B
-                // image): the 6-wave kernel; fewer: the 5-wave kernel (1/2 and
-                // 1/4 slabs: 3-4 % faster than 6 waves there); fewer items than
-                // 5-wave lanes (a 1/8 slab: 259k pixels, 327k lanes): every lane
-                // owns at most one long item, so the split-wave kernel traces
-                // each 64 rays with S waves (1/S of the triangles each)
-                auto lanes = [&](int v, unsigned long long& out) -> int {
-                    int occ0 = 0;
-                    HIPCHECK(kVariants[v].occupancy(&occ0, 0));
-                    out = (unsigned long long)s->num_cus * (unsigned long long)std::max(occ0, 1) * kVariants[v].block;
-                    return 0;
-                };
-                unsigned long long lanes6 = 0, lanes5 = 0;
-                if (lanes(0, lanes6) < 0 || lanes(kMidSlabVariant, lanes5) < 0) return -1;
-                if (p.n_items < lanes5)
-                    vi = kSmallSlabVariant;
-                else if (p.n_items < 4 * lanes6)
-                    vi = kMidSlabVariant;
-            }
+    // explicit variant (rt2_scene_set_variant) when it exists in this build and
+    // matches the traversal; otherwise the automatic choice: scalar-path kernel
+    // for small scenes (config B: 1,208 triangles), LDS-tiled sweep for large
+    // ones (config E: 1M triangles)
+    const Variant* VP = s->variant > 0 ? find_variant(s->variant) : nullptr;
+    if (VP && ((s->traversal == RT2_TRAVERSAL_BVH) != (VP->kind >= K_BVH))) VP = nullptr;
+    if (VP && VP->kind == K_RESIDENT && !fits) VP = nullptr;  // cannot hold this scene
+    if (!VP && s->traversal == RT2_TRAVERSAL_BVH) VP = find_variant(kDefaultBvh);
+    if (!VP) {
+        int vi = s->n_tris <= kSmemMaxTris ? kDefaultBrute : kLargeScene;
+        if (vi == kDefaultBrute) {
+            // items per resident lane decide the tail: a lane ends on a
+            // whole item, so with few items per lane the last round runs
+            // partly empty.  >= 4 per lane at 6 waves/SIMD (a full config B
+            // image): the 6-wave kernel; fewer: the 5-wave kernel (1/2 and
+            // 1/4 slabs: 3-4 % faster than 6 waves there); fewer items than
+            // 5-wave lanes (a 1/8 slab: 259k pixels, 327k lanes): every lane
+            // owns at most one long item, so the split-wave kernel traces
+            // each 64 rays with S waves (1/S of the triangles each)
+            auto lanes = [&](int v, unsigned long long& out) -> int {
+                const Variant* W = find_variant(v);
+                int occ0 = 0;
+                HIPCHECK(variant_occupancy(*W, &occ0, 0));
+                out = (unsigned long long)s->num_cus * (unsigned long long)std::max(occ0, 1) * W->block;
+                return 0;
+            };
+            unsigned long long lanes6 = 0, lanes5 = 0;
+            if (lanes(kDefaultBrute, lanes6) < 0 || lanes(kMidSlab, lanes5) < 0) return -1;
+            if (p.n_items < lanes5)
+                vi = kSmallSlab;
+            else if (p.n_items < 4 * lanes6)
+                vi = kMidSlab;
         }
-        if (kVariants[vi].kind == K_RESIDENT && !fits) vi = kLargeSceneVariant;  // cannot hold this scene
+        VP = find_variant(vi);
     }
-    const Variant& V = kVariants[vi];
+    const Variant& V = *VP;
     size_t lds = 0;
     if (V.kind == K_TILED)
         lds = (size_t)3 * sizeof(float4) * kTileTris;
@@ -806,13 +789,13 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     p.recs_ok = s->recs_ok;
     s->last_kind = V.kind >= K_BVH ? K_BVH : V.kind;
     int occ = 0;
-    HIPCHECK(V.occupancy(&occ, lds));
+    HIPCHECK(variant_occupancy(V, &occ, lds));
     occ = std::max(occ, 1);
     unsigned long long blocks = (unsigned long long)s->num_cus * occ;
     const int rays_per_block = V.kind == K_SPLIT ? 64 : V.block;  // split: S waves per 64 rays
     blocks = std::min(blocks, (p.n_items + rays_per_block - 1) / rays_per_block);
     blocks = std::max(blocks, 1ull);
-    s->last_variant = vi;
+    s->last_variant = V.id;
     HIPCHECK(V.launch(p, (int)blocks, lds, st));
     HIPCHECK(hipGetLastError());
     if (p.frame_split) {
@@ -878,6 +861,29 @@ extern "C" int rt2_resolve_rgb8_reference(const uint32_t* acc8, int64_t n, uint3
     return 0;
 }
 
+// Grows the scene's render_host buffers to `n` pixels.  On failure the
+// buffers stay owned by the scene (freed by rt2_scene_destroy): no leak on any
+// error path.
+static int host_buffers(rt2_scene* s, size_t n) {
+    if (!s->host_stream) HIPCHECK(hipStreamCreateWithFlags(&s->host_stream, hipStreamNonBlocking));
+    if (n <= s->host_cap) return 0;
+    HIPCHECK(hipStreamSynchronize(s->host_stream));
+    (void)hipFree(s->d_host_acc);
+    (void)hipFree(s->d_host_res);
+    (void)hipFree(s->d_host_acc8);
+    (void)hipFree(s->d_host_rgb8);
+    s->d_host_acc = s->d_host_res = nullptr;
+    s->d_host_acc8 = nullptr;
+    s->d_host_rgb8 = nullptr;
+    s->host_cap = 0;
+    HIPCHECK(hipMalloc(&s->d_host_acc, n * sizeof(float4)));
+    HIPCHECK(hipMalloc(&s->d_host_res, n * sizeof(float4)));
+    HIPCHECK(hipMalloc(&s->d_host_acc8, n * sizeof(uint4)));
+    HIPCHECK(hipMalloc(&s->d_host_rgb8, n * 3));
+    s->host_cap = n;
+    return 0;
+}
+
 extern "C" int rt2_render_host(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_begin, uint32_t frame_count,
                                rt2_shard sh, float* out_rgba, uint8_t* out_rgb8) {
     if (!s || !u) {
@@ -890,47 +896,29 @@ extern "C" int rt2_render_host(rt2_scene* s, const rt2_uniforms* u, uint32_t fra
         return -1;
     }
     const size_t n = (size_t)rows * u->width;
+    if (n == 0 || frame_count == 0) return 0;
     HIPCHECK(hipSetDevice(s->device));
-    float* acc = nullptr;
-    float* res = nullptr;
-    uint32_t* acc8 = nullptr;
-    HIPCHECK(hipMalloc(&acc, std::max(n, (size_t)1) * 16));
-    HIPCHECK(hipMalloc(&res, std::max(n, (size_t)1) * 16));
-    HIPCHECK(hipMemset(acc, 0, std::max(n, (size_t)1) * 16));
+    if (host_buffers(s, n) != 0) return -1;
+    hipStream_t st = s->host_stream;
+    HIPCHECK(hipMemsetAsync(s->d_host_acc, 0, n * sizeof(float4), st));
+    if (out_rgb8) HIPCHECK(hipMemsetAsync(s->d_host_acc8, 0, n * sizeof(uint4), st));
+    if (rt2_render(s, u, frame_begin, frame_count, sh, reinterpret_cast<float*>(s->d_host_acc),
+                   out_rgb8 ? reinterpret_cast<uint32_t*>(s->d_host_acc8) : nullptr, st) != 0)
+        return -1;
+    if (out_rgba) {
+        if (rt2_resolve_rgba32f(reinterpret_cast<const float*>(s->d_host_acc), (int64_t)n, frame_count,
+                                reinterpret_cast<float*>(s->d_host_res), st) != 0)
+            return -1;
+        HIPCHECK(hipMemcpyAsync(out_rgba, s->d_host_res, n * sizeof(float4), hipMemcpyDeviceToHost, st));
+    }
     if (out_rgb8) {
-        HIPCHECK(hipMalloc(&acc8, std::max(n, (size_t)1) * 16));
-        HIPCHECK(hipMemset(acc8, 0, std::max(n, (size_t)1) * 16));
+        hipLaunchKernelGGL(resolve_rgb8_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                           s->d_host_acc8, (long long)n, (float)frame_count, s->d_host_rgb8);
+        HIPCHECK(hipGetLastError());
+        HIPCHECK(hipMemcpyAsync(out_rgb8, s->d_host_rgb8, n * 3, hipMemcpyDeviceToHost, st));
     }
-    int rc = rt2_render(s, u, frame_begin, frame_count, sh, acc, acc8, nullptr);
-    if (rc == 0 && out_rgba && n) {
-        rc = rt2_resolve_rgba32f(acc, (int64_t)n, frame_count, res, nullptr);
-        if (rc == 0) {
-            hipError_t e = hipMemcpy(out_rgba, res, n * 16, hipMemcpyDeviceToHost);
-            if (e != hipSuccess) {
-                rt2h::set_error(std::string("hipMemcpy: ") + hipGetErrorString(e));
-                rc = -1;
-            }
-        }
-    }
-    if (rc == 0 && out_rgb8 && n) {
-        std::vector<uint32_t> h8(n * 4);
-        hipError_t e = hipMemcpy(h8.data(), acc8, n * 16, hipMemcpyDeviceToHost);
-        if (e != hipSuccess) {
-            rt2h::set_error(std::string("hipMemcpy: ") + hipGetErrorString(e));
-            rc = -1;
-        } else {
-            rc = rt2_resolve_rgb8_reference(h8.data(), (int64_t)n, frame_count, out_rgb8);
-        }
-    }
-    hipError_t e = hipDeviceSynchronize();
-    if (rc == 0 && e != hipSuccess) {
-        rt2h::set_error(std::string("render: ") + hipGetErrorString(e));
-        rc = -1;
-    }
-    (void)hipFree(acc);
-    (void)hipFree(res);
-    (void)hipFree(acc8);
-    return rc;
+    HIPCHECK(hipStreamSynchronize(st));  // only this render's stream, not the device
+    return 0;
 }
 
 // Not in rt2.h (diagnostics): counters of the last rt2_scene_stats call

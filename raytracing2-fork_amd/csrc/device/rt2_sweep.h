@@ -1,10 +1,26 @@
 // Kernel parameters, per-lane helpers and the closest-hit sweeps of the brute
-// path: Möller–Trumbore (compute.glsl:354-381) exact and filtered, the
-// SMEM/LDS/ballot/min-filter/cooperative sweeps and their dispatch.
+// path: Möller–Trumbore (compute.glsl:302-340) behind an exact filter, the
+// scalar-cache / LDS sweeps, the cooperative drain and the named kernel specs.
 // Included by rt2_render.hip only (one translation unit; internal linkage).
 #pragma once
 
 namespace {
+
+// Division-free filter evaluated before the reference arithmetic (DESIGN.md,
+// "Exactness of the filter"); every form only skips tests the reference
+// would reject, so all give the same bits.
+enum class Filter : int {
+    Five = 0,  // mt_pass: five compares and an and-chain
+    Max3 = 1,  // mt_pass3: two v_max3_f32 and one compare (default)
+    Plk = 2,   // per-ray precomputed records (sweep_plk; experiment builds)
+};
+
+// What a wave does when the item pool is empty and few of its lanes still trace.
+enum class Tail : int {
+    None = 0,  // every lane sweeps its own ray
+    Coop = 1,  // the whole wave computes each live ray's closest hit (coop_closest)
+    Team = 2,  // k = 64 / 2^ceil(log2 live) lanes per live ray (team_closest)
+};
 
 struct RenderParams {
     const float4* tri;  // 3 float4 per triangle: {ax ay az e0x} {e0y e0z e1x e1y} {e1z nx ny nz}
@@ -87,172 +103,6 @@ struct FiltStats {
     }
 };
 
-// One Möller–Trumbore test (compute.glsl:302-340) against a pre-transformed
-// triangle; updates the running closest hit (compute.glsl:432-434).
-__device__ __forceinline__ void mt_test(const f3& o, const f3& d, float4 t0, float4 t1, float4 t2, int idx,
-                                        float& best, int& best_i) {
-    const f3 a = mk(t0.x, t0.y, t0.z);
-    const f3 e0 = mk(t0.w, t1.x, t1.y);
-    const f3 e1 = mk(t1.z, t1.w, t2.x);
-    const f3 n = mk(t2.y, t2.z, t2.w);
-    float det = -dot(d, n);
-    bool ok = !((det < 1e-10f && det > -1e-10f) || det < 0.0f);
-    float inv = 1.0f / det;
-    f3 ao = sub(o, a);
-    float dst = dot(ao, n) * inv;
-    ok = ok && !(dst <= 1e-6f);
-    f3 q = cross(d, ao);
-    float u = -dot(e1, q) * inv;
-    float v = dot(e0, q) * inv;
-    ok = ok && !(u < 0.0f || v < 0.0f || 1.0f - u - v < 0.0f);
-    if (ok && dst < best) {
-        best = dst;
-        best_i = idx;
-    }
-}
-
-// Filtered Möller–Trumbore: same decision as mt_test, bit for bit.
-//
-// With det = -dot(d,n), inv = RN(1/det), the reference updates the closest hit
-// iff det >= 1e-10, dst = RN(tnum*inv) > 1e-6, u = RN(-U*inv) >= 0,
-// v = RN(V*inv) >= 0, RN(RN(1-u)-v) >= 0 and dst < best, where tnum =
-// dot(o-a, n), U = dot(e1, q), V = dot(e0, q), q = cross(d, o-a).  The filter
-// F below uses only those exact intermediates (no division) and is false only
-// when the update is impossible ("Exactness of the
-// filter"): for det > 0, inv > 0, so
-//   tnum <= 0                      => dst <= 0                (reject)
-//   U > det*2^-60                  => u <= -2^-61 < 0         (reject)
-//   V < -det*2^-60                 => v < 0                   (reject)
-//   RN(V-U) > RN(det*(1+2^-10))    => w < 0 (u, v >= -2^-60)  (reject)
-//   tnum > RN(det*RN(best*(1+2^-10))) => dst >= best          (no update)
-// det < 0, det = 0 and NaN fail `tnum > 0 && tnum <= det*bestK`; 0 < det <
-// 1e-10 and det = +inf pass F and are rejected by the exact path, as in the
-// reference.  Only F-survivors (a few per mille of pairs) pay for the IEEE
-// division.
-__device__ __forceinline__ void mt_test_filtered(const f3& o, const f3& d, float4 t0, float4 t1, float4 t2, int idx,
-                                                 float& best, int& best_i, float& bestK) {
-    const f3 a = mk(t0.x, t0.y, t0.z);
-    const f3 e0 = mk(t0.w, t1.x, t1.y);
-    const f3 e1 = mk(t1.z, t1.w, t2.x);
-    const f3 n = mk(t2.y, t2.z, t2.w);
-    const float det = -dot(d, n);
-    const f3 ao = sub(o, a);
-    const float tnum = dot(ao, n);
-    const f3 q = cross(d, ao);
-    const float U = dot(e1, q);
-    const float V = dot(e0, q);
-    const float B = det * 0x1p-60f;
-    const bool F = (tnum > 0.0f) & (U <= B) & (V >= -B) & ((V - U) <= det * 1.0009765625f) & (tnum <= det * bestK);
-    if (F) {
-        // compute.glsl:312-327, exactly as written
-        if (!((det < 1e-10f && det > -1e-10f) || det < 0.0f)) {
-            const float inv = 1.0f / det;
-            const float dst = tnum * inv;
-            const float u = -U * inv;
-            const float v = V * inv;
-            if (!(dst <= 1e-6f) && !(u < 0.0f || v < 0.0f || 1.0f - u - v < 0.0f) && dst < best) {
-                best = dst;
-                best_i = idx;
-                bestK = best * 1.0009765625f;
-            }
-        }
-    }
-}
-
-// Filter part of mt_test_filtered only (branch-free): true when triangle
-// {t0,t1,t2} may update the closest hit.
-__device__ __forceinline__ bool mt_filter(const f3& o, const f3& d, float4 t0, float4 t1, float4 t2, float bestK) {
-    const f3 a = mk(t0.x, t0.y, t0.z);
-    const f3 e0 = mk(t0.w, t1.x, t1.y);
-    const f3 e1 = mk(t1.z, t1.w, t2.x);
-    const f3 n = mk(t2.y, t2.z, t2.w);
-    const float det = -dot(d, n);
-    const f3 ao = sub(o, a);
-    const float tnum = dot(ao, n);
-    const f3 q = cross(d, ao);
-    const float U = dot(e1, q);
-    const float V = dot(e0, q);
-    const float B = det * 0x1p-60f;
-    return (tnum > 0.0f) & (U <= B) & (V >= -B) & ((V - U) <= det * 1.0009765625f) & (tnum <= det * bestK);
-}
-
-// Two-phase sweep over [begin, end) of the LDS array (triangle indices base+k):
-// phase 1 evaluates the filter of G triangles branch-free (G independent
-// dependency chains, 3G LDS reads in flight), phase 2 runs the exact test
-// (mt_test_filtered) for the surviving bits in increasing index order — the
-// same update sequence as testing every triangle in order.
-// Diagnostic counters of the grouped sweep (STATS variants only).
-struct SweepStats {
-    uint32_t groups = 0;         // phase-1 groups evaluated (per wave)
-    uint32_t groups_exact = 0;   // groups where some lane had a survivor (per wave)
-    uint32_t exact_iters = 0;    // phase-2 iterations executed by the wave
-    uint32_t lane_survivors = 0; // survivor bits summed over lanes
-};
-
-template <int G, bool STATS = false>
-__device__ __forceinline__ void sweep_grouped(const f3& o, const f3& d, const float4* lds, int count, int base,
-                                              float& best, int& bi, float& bestK, SweepStats* ss = nullptr) {
-    int i = 0;
-    for (; i + G <= count; i += G) {
-        uint32_t m = 0;
-#pragma unroll
-        for (int k = 0; k < G; k++) {
-            const float4* t = lds + 3 * (i + k);
-            m |= (uint32_t)mt_filter(o, d, t[0], t[1], t[2], bestK) << k;
-        }
-        if constexpr (STATS) {
-            ss->groups += 1;
-            ss->lane_survivors += __popc(m);
-            if (__any(m != 0)) ss->groups_exact += 1;
-            uint32_t mm = m;
-            while (__any(mm != 0)) {
-                ss->exact_iters += 1;
-                mm &= mm - 1;
-            }
-        }
-        while (m) {
-            const int k = __builtin_ctz(m);
-            m &= m - 1;
-            const float4* t = lds + 3 * (i + k);
-            mt_test_filtered(o, d, t[0], t[1], t[2], base + i + k, best, bi, bestK);
-        }
-    }
-    for (; i < count; i++) {
-        const float4* t = lds + 3 * i;
-        mt_test_filtered(o, d, t[0], t[1], t[2], base + i, best, bi, bestK);
-    }
-}
-
-// Scalar-path sweep: the triangle records are wave-uniform, so they are read
-// with scalar loads (constant address space -> s_load_dwordx4 into SGPRs,
-// through the scalar cache) and fed to the VALU as SGPR operands; no LDS, no
-// VGPRs for triangle data.  Same two-phase structure as sweep_grouped.
-typedef const __attribute__((address_space(4))) float cfloat;
-__device__ __forceinline__ float4 ldc4(cfloat* p) { return make_float4(p[0], p[1], p[2], p[3]); }
-template <int G>
-__device__ __forceinline__ void sweep_smem(const f3& o, const f3& d, cfloat* tri, int count, float& best, int& bi,
-                                           float& bestK) {
-    int i = 0;
-    for (; i + G <= count; i += G) {
-        uint32_t m = 0;
-#pragma unroll
-        for (int k = 0; k < G; k++) {
-            cfloat* t = tri + 12 * (i + k);
-            m |= (uint32_t)mt_filter(o, d, ldc4(t), ldc4(t + 4), ldc4(t + 8), bestK) << k;
-        }
-        while (m) {
-            const int k = __builtin_ctz(m);
-            m &= m - 1;
-            cfloat* t = tri + 12 * (i + k);
-            mt_test_filtered(o, d, ldc4(t), ldc4(t + 4), ldc4(t + 8), i + k, best, bi, bestK);
-        }
-    }
-    for (; i < count; i++) {
-        cfloat* t = tri + 12 * i;
-        mt_test_filtered(o, d, ldc4(t), ldc4(t + 4), ldc4(t + 8), i, best, bi, bestK);
-    }
-}
-
 // Exact intermediates of one test (phase 1 output, reused by phase 2).
 struct MtQ {
     float det, tnum, U, V;
@@ -293,13 +143,19 @@ __device__ __forceinline__ bool mt_pass3(const MtQ& q, float bestK) {
     const float Y = __builtin_fmaf(-q.det, bestK, q.tnum);
     return fmaxf(fmaxf(fmaxf(fmaxf(q.U, -q.V), X), -q.tnum), Y) <= B;
 }
-template <int FILT>
+template <Filter FILT>
 __device__ __forceinline__ bool mt_pass_f(const MtQ& q, float bestK) {
-    if constexpr (FILT == 1)
+    if constexpr (FILT == Filter::Max3)
         return mt_pass3(q, bestK);
     else
         return mt_pass(q, bestK);
 }
+
+// Scalar-path record delivery: a triangle record is wave-uniform, so it is read
+// with scalar loads (constant address space -> s_load_dwordx4 into SGPRs,
+// through the scalar data cache) and fed to the VALU as SGPR operands.
+typedef const __attribute__((address_space(4))) float cfloat;
+__device__ __forceinline__ float4 ldc4(cfloat* p) { return make_float4(p[0], p[1], p[2], p[3]); }
 
 // compute.glsl:312-327 on the phase-1 intermediates (exactly the reference arithmetic).
 __device__ __forceinline__ void mt_exact(const MtQ& q, int idx, float& best, int& bi, float& bestK) {
@@ -321,7 +177,7 @@ __device__ __forceinline__ void mt_exact(const MtQ& q, int idx, float& best, int
 // per-lane bit packing); phase 2 runs mt_exact under each mask in index order
 // (skipped by a scalar branch when the mask is empty).  SMEM selects the
 // scalar-load path for the triangle records instead of LDS.
-template <int G, bool SMEM, int FILT = 0, bool STATS = false>
+template <int G, bool SMEM, Filter FILT = Filter::Five, bool STATS = false>
 __device__ __forceinline__ void sweep_masked(const f3& o, const f3& d, const float4* lds, const float* gtri,
                                              int count, int base, float& best, int& bi, float& bestK,
                                              FiltStats* fs = nullptr) {
@@ -442,138 +298,6 @@ __device__ __forceinline__ bool plk_lane_ok(const f3& o, const f3& d) {
     return O <= 0x1p20f && D <= 1.0001f;  // false for NaN and inf
 }
 
-// Ballot sweep: phase 1 computes G filters and turns them into wave masks
-// (__ballot); phase 2 runs only when any mask is set, one scalar branch per G
-// triangles in the common case.
-__device__ __forceinline__ void load_tri_smem(const float* gtri, int i, float4& t0, float4& t1, float4& t2) {
-    cfloat* t = (cfloat*)gtri + 12 * i;
-    t0 = ldc4(t);
-    t1 = ldc4(t + 4);
-    t2 = ldc4(t + 8);
-}
-template <int G>
-__device__ __forceinline__ void sweep_ballot(const f3& o, const f3& d, const float* gtri, int count, float& best,
-                                             int& bi, float& bestK) {
-    int i = 0;
-    const unsigned long long me = 1ull << lane_id();
-    for (; i + G <= count; i += G) {
-        MtQ q[G];
-        unsigned long long m[G], any = 0;
-#pragma unroll
-        for (int k = 0; k < G; k++) {
-            float4 t0, t1, t2;
-            load_tri_smem(gtri, i + k, t0, t1, t2);
-            q[k] = mt_quantities(o, d, t0, t1, t2);
-            m[k] = __ballot(mt_pass(q[k], bestK));
-            any |= m[k];
-        }
-        if (__builtin_expect(any != 0, 0)) {
-#pragma unroll
-            for (int k = 0; k < G; k++)
-                if (m[k] & me) mt_exact(q[k], i + k, best, bi, bestK);
-        }
-    }
-    for (; i < count; i++) {
-        float4 t0, t1, t2;
-        load_tri_smem(gtri, i, t0, t1, t2);
-        const MtQ q = mt_quantities(o, d, t0, t1, t2);
-        if (mt_pass(q, bestK)) mt_exact(q, i, best, bi, bestK);
-    }
-}
-
-// VALU-only form of mt_pass: the five conditions as signed slacks whose
-// minimum is >= 0 exactly when all hold (RN(x - y) has the sign of x - y;
-// tnum > 0 as tnum - 2^-149 >= 0).  Conservative under flush-to-zero and NaN
-// as well (both can only make it pass more).
-__device__ __forceinline__ bool mt_pass_min(const MtQ& q, float bestK) {
-    const float B = q.det * 0x1p-60f;
-    const float D = q.det * 1.0009765625f;
-    const float K = q.det * bestK;
-    const float m1 = fminf(fminf(B - q.U, q.V + B), D - (q.V - q.U));
-    const float m2 = fminf(K - q.tnum, q.tnum - 0x1p-149f);
-    return fminf(m1, m2) >= 0.0f;
-}
-template <int G>
-__device__ __forceinline__ void sweep_minfilter(const f3& o, const f3& d, const float* gtri, int count, float& best,
-                                                int& bi, float& bestK) {
-    int i = 0;
-    const unsigned long long me = 1ull << lane_id();
-    for (; i + G <= count; i += G) {
-        MtQ q[G];
-        unsigned long long m[G], any = 0;
-#pragma unroll
-        for (int k = 0; k < G; k++) {
-            float4 t0, t1, t2;
-            load_tri_smem(gtri, i + k, t0, t1, t2);
-            q[k] = mt_quantities(o, d, t0, t1, t2);
-            m[k] = __ballot(mt_pass_min(q[k], bestK));
-            any |= m[k];
-        }
-        if (__builtin_expect(any != 0, 0)) {
-#pragma unroll
-            for (int k = 0; k < G; k++)
-                if (m[k] & me) mt_exact(q[k], i + k, best, bi, bestK);
-        }
-    }
-    for (; i < count; i++) {
-        float4 t0, t1, t2;
-        load_tri_smem(gtri, i, t0, t1, t2);
-        const MtQ q = mt_quantities(o, d, t0, t1, t2);
-        if (mt_pass(q, bestK)) mt_exact(q, i, best, bi, bestK);
-    }
-}
-
-// Lean masked sweep: like sweep_masked, but phase 1 keeps ONLY the G filter
-// lane-masks (SGPRs) live; phase 2 (entered for ~5% of groups on config B)
-// reloads the surviving triangle and recomputes its intermediates.  Frees the
-// 4*G VGPRs sweep_masked holds across the group.
-__device__ __forceinline__ void load_tri(const float4* lds, const float* gtri, bool smem, int i, float4& t0,
-                                         float4& t1, float4& t2) {
-    if (smem) {
-        cfloat* t = (cfloat*)gtri + 12 * i;
-        t0 = ldc4(t);
-        t1 = ldc4(t + 4);
-        t2 = ldc4(t + 8);
-    } else {
-        const float4* t = lds + 3 * i;
-        t0 = t[0];
-        t1 = t[1];
-        t2 = t[2];
-    }
-}
-template <int G, bool SMEM>
-__device__ __forceinline__ void sweep_lean(const f3& o, const f3& d, const float4* lds, const float* gtri, int count,
-                                           int base, float& best, int& bi, float& bestK) {
-    int i = 0;
-    for (; i + G <= count; i += G) {
-        bool f[G];
-#pragma unroll
-        for (int k = 0; k < G; k++) {
-            float4 t0, t1, t2;
-            load_tri(lds, gtri, SMEM, i + k, t0, t1, t2);
-            f[k] = mt_pass(mt_quantities(o, d, t0, t1, t2), bestK);
-        }
-#pragma unroll
-        for (int k = 0; k < G; k++) {
-            if (f[k]) {
-                // opaque index: force a reload + recompute instead of keeping
-                // phase 1's intermediates live across the group
-                int j = i + k;
-                asm volatile("" : "+s"(j));
-                float4 t0, t1, t2;
-                load_tri(lds, gtri, SMEM, j, t0, t1, t2);
-                mt_exact(mt_quantities(o, d, t0, t1, t2), base + j, best, bi, bestK);
-            }
-        }
-    }
-    for (; i < count; i++) {
-        float4 t0, t1, t2;
-        load_tri(lds, gtri, SMEM, i, t0, t1, t2);
-        const MtQ q = mt_quantities(o, d, t0, t1, t2);
-        if (mt_pass(q, bestK)) mt_exact(q, base + i, best, bi, bestK);
-    }
-}
-
 // Cooperative closest hit for the drain phase: all 64 lanes sweep ONE ray
 // (lane l tests triangles l, l+64, ... in increasing order with its own
 // running best) and the wave reduces (dst, index) lexicographically.  The
@@ -650,15 +374,6 @@ __device__ __forceinline__ void team_closest(const f3& lo, const f3& ld, const f
     const int src = (int)lanes_below(act) * k;
     best_out = __shfl(best, src);
     bi_out = __shfl(bi, src);
-}
-
-template <int MT>
-__device__ __forceinline__ void mt_dispatch(const f3& o, const f3& d, float4 t0, float4 t1, float4 t2, int idx,
-                                            float& best, int& best_i, float& bestK) {
-    if constexpr (MT == 0)
-        mt_test(o, d, t0, t1, t2, idx, best, best_i);
-    else
-        mt_test_filtered(o, d, t0, t1, t2, idx, best, best_i, bestK);
 }
 
 }  // namespace

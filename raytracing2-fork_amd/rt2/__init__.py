@@ -28,7 +28,9 @@ from typing import Optional, Sequence
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librt2.so")
+# RT2_LIB=exp selects the experiment build (make EXPERIMENTS=1: the product
+# kernels plus the A/B variants of DESIGN.md "Tried and measured").
+LIB_PATH = os.path.join(_HERE, "librt2_exp.so" if os.environ.get("RT2_LIB") == "exp" else "librt2.so")
 
 DIFFUSE, SPECULAR, LIGHT, CHECKER, GLASS, TEXTURE, GLASS_HIGHLIGHT = range(7)
 
@@ -118,7 +120,8 @@ class Shard(C.Structure):
     _fields_ = [("tile_rows", C.c_int32), ("rank", C.c_int32), ("nranks", C.c_int32)]
 
 
-ABI_VERSION = 3  # include/rt2.h RT2_ABI_VERSION
+ABI_VERSION = 4  # include/rt2.h RT2_ABI_VERSION
+COMM_ID_BYTES = 128  # RT2_COMM_ID_BYTES
 
 
 class Image(C.Structure):
@@ -164,7 +167,8 @@ EXPORTED = [
     "rt2_material_default", "rt2_material_make_diffuse", "rt2_material_make_light", "rt2_material_make_specular",
     "rt2_material_make_checker", "rt2_material_make_glass", "rt2_camera_default", "rt2_camera_uniforms",
     "rt2_uniforms_offline", "rt2_write_png", "rt2_image_load", "rt2_image_free", "rt2_sd_texture",
-    "rt2_scene_set_textures",
+    "rt2_scene_set_textures", "rt2_comm_unique_id", "rt2_comm_init", "rt2_comm_wrap", "rt2_comm_destroy",
+    "rt2_comm_size", "rt2_comm_check", "rt2_gather_slabs", "rt2_unshard_slabs", "rt2_render_host_gather",
 ]
 
 _lib: Optional[C.CDLL] = None
@@ -248,6 +252,15 @@ def lib() -> C.CDLL:
         "rt2_camera_uniforms": (C.c_int, [C.POINTER(CameraDesc), C.POINTER(Uniforms)]),
         "rt2_uniforms_offline": (None, [C.POINTER(Uniforms), I32, I32, I32, I32, I32, I32]),
         "rt2_write_png": (C.c_int, [C.c_char_p, I32, I32, I32, P, I32]),
+        "rt2_comm_unique_id": (C.c_int, [P]),
+        "rt2_comm_init": (C.c_int, [P, I32, I32, I32, C.POINTER(P)]),
+        "rt2_comm_wrap": (C.c_int, [P, I32, C.POINTER(P)]),
+        "rt2_comm_destroy": (None, [P]),
+        "rt2_comm_size": (C.c_int, [P, C.POINTER(I32), C.POINTER(I32)]),
+        "rt2_comm_check": (C.c_int, [P]),
+        "rt2_gather_slabs": (C.c_int, [P, P, I32, I32, Shard, I32, P, P]),
+        "rt2_unshard_slabs": (C.c_int, [P, I32, I32, I32, Shard, P, P]),
+        "rt2_render_host_gather": (C.c_int, [P, C.POINTER(Uniforms), U32, U32, Shard, P, I32, P, P]),
         "rt2_device_selftest": (C.c_int, [P, I32, P]),
         "rt2_device_rcp_check": (C.c_int, [U32, U32, C.c_int, C.POINTER(C.c_ulonglong), C.POINTER(U32)]),
         "rt2_device_div_check": (C.c_int, [U32, C.c_ulonglong, C.c_int, C.POINTER(C.c_ulonglong), C.POINTER(U32)]),
@@ -429,6 +442,52 @@ def shard_row_ids(height: int, sh: Shard) -> np.ndarray:
     return np.array([lib().rt2_shard_row(i, sh) for i in range(n)], dtype=np.int32)
 
 
+class Comm:
+    """RCCL communicator of the multi-GPU C-ABI (rt2_comm_*): one per rank/GPU."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (C.c_uint8 * COMM_ID_BYTES)()
+        _check(lib().rt2_comm_unique_id(buf), "rt2_comm_unique_id")
+        return bytes(buf)
+
+    def __init__(self, uid: bytes, nranks: int, rank: int, device: int = 0):
+        if len(uid) != COMM_ID_BYTES:
+            raise RT2Error(f"communicator id must be {COMM_ID_BYTES} bytes")
+        buf = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid)
+        p = C.c_void_p()
+        _check(lib().rt2_comm_init(buf, nranks, rank, device, C.byref(p)), "rt2_comm_init")
+        self._p = p
+        self.nranks, self.rank, self.device = nranks, rank, device
+
+    def close(self):
+        if getattr(self, "_p", None) and _lib is not None:
+            _lib.rt2_comm_destroy(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown
+            pass
+
+    def check(self) -> None:
+        _check(lib().rt2_comm_check(self._p), "rt2_comm_check")
+
+    def gather_slabs(self, slab_ptr: int, width: int, height: int, sh: Shard, root: int, image_ptr: int,
+                     stream: int = 0) -> None:
+        _check(lib().rt2_gather_slabs(self._p, C.c_void_p(slab_ptr), width, height, sh, root,
+                                      C.c_void_p(image_ptr) if image_ptr else None,
+                                      C.c_void_p(stream) if stream else None), "rt2_gather_slabs")
+
+
+def unshard_slabs(gathered_ptr: int, max_rows: int, width: int, height: int, layout: Shard, image_ptr: int,
+                  stream: int = 0) -> None:
+    """Root-side un-interleave of [nranks][max_rows][width] 16-byte pixels (rt2_unshard_slabs)."""
+    _check(lib().rt2_unshard_slabs(C.c_void_p(gathered_ptr), max_rows, width, height, layout, C.c_void_p(image_ptr),
+                                   C.c_void_p(stream) if stream else None), "rt2_unshard_slabs")
+
+
 class Scene:
     """Device-resident scene: the SSBO uploads of rayTracing.cpp:1323-1325."""
 
@@ -459,7 +518,11 @@ class Scene:
             pass
 
     def set_variant(self, v: int) -> int:
-        return lib().rt2_scene_set_variant(self._p, v)
+        """Forces kernel variant v (0 = automatic); raises if v is not in this build."""
+        r = lib().rt2_scene_set_variant(self._p, v)
+        if r < 0:
+            _check(r, "set_variant")
+        return r
 
     def set_traversal(self, traversal: str) -> None:
         """"brute" (north-star kernel) or "bvh" (compute.glsl:410-460 on the uploaded nodes)."""
@@ -502,10 +565,30 @@ class Scene:
                                      None if out8 is None else out8.ctypes.data), "rt2_render_host")
         return (out, out8) if rgb8 else out
 
+    def render_host_gather(self, u: Uniforms, frame_begin: int, frame_count: int, sh: Shard, comm: "Comm",
+                           root: int = 0, rgb8: bool = False):
+        """rt2_render_host_gather: this rank's shard, gathered to `root`; returns the
+        whole (H, W, 4) mean image [and the 8-bit average] on the root, None elsewhere."""
+        is_root = comm.rank == root
+        out = np.zeros((u.height, u.width, 4), dtype=np.float32) if is_root else None
+        out8 = np.zeros((u.height, u.width, 3), dtype=np.uint8) if (is_root and rgb8) else None
+        _check(lib().rt2_render_host_gather(self._p, C.byref(u), frame_begin, frame_count, sh, comm._p, root,
+                                            None if out is None else out.ctypes.data,
+                                            None if out8 is None else out8.ctypes.data), "rt2_render_host_gather")
+        if not is_root:
+            return None
+        return (out, out8) if rgb8 else out
+
     def stats(self, reset: bool = False) -> Stats:
         s = Stats()
         _check(lib().rt2_scene_stats(self._p, C.byref(s), int(reset)), "stats")
         return s
+
+
+def has_variant(v: int) -> bool:
+    """Whether kernel variant v is compiled into the loaded library (experiment
+    variants need make EXPERIMENTS=1 and RT2_LIB=exp)."""
+    return v == 0 or lib().rt2_variant_name(v) is not None
 
 
 def resolve_rgba32f(accum_ptr: int, n_pixels: int, frames: int, out_ptr: int, stream: int = 0) -> None:

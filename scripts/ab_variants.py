@@ -1,6 +1,8 @@
 """A/B of kernel variants in ONE process, interleaved rounds (cdna guide §5.4 rule 24).
 Renders a configuration with each variant, checks every variant's image is
-bit-identical to variant 1 (the round-1 kernel), reports median / min ms."""
+bit-identical to the first variant's, reports median / min ms.  Experiment
+variants need the experiment build: make -C raytracing2-fork_amd EXPERIMENTS=1
+and RT2_LIB=exp in the environment."""
 import argparse
 import json
 import os
@@ -16,7 +18,7 @@ import rt2  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="B")
-ap.add_argument("--variants", default="1,3,0,4,5,6,2,7,8")
+ap.add_argument("--variants", default="0,67")
 ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--width", type=int, default=0)
 ap.add_argument("--height", type=int, default=0)

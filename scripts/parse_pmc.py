@@ -9,11 +9,23 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
+sys.path.insert(0, ROOT)
+from bench import kernel_source_digest  # noqa: E402
+
+
+def bench_variant(name):
+    """The kernel variant the profiled bench run launched (its JSON line)."""
+    for line in reversed(open(os.path.join(OUT, f"pmc_{name}.log")).read().splitlines()):
+        if line.startswith("{"):
+            m = re.search(r"variant ([^)]+)\)", json.loads(line)["roofline"]["kernel"] or "")
+            return m.group(1) if m else None
+    return None
 
 
 def load(name):
@@ -36,7 +48,8 @@ def main(config="B"):
     res = {}
     for name in ("fetch", "write", "valu", "salu", "clock", "wait"):
         res.update(load(name))
-    out = {"config": config, "counters_per_launch": res}
+    out = {"config": config, "kernel_variant": bench_variant("fetch"),
+           "kernel_source_sha256": kernel_source_digest(), "counters_per_launch": res}
     if "FETCH_SIZE" in res and "WRITE_SIZE" in res:
         out["hbm_bytes_per_launch"] = int((2 * res["FETCH_SIZE"] + res["WRITE_SIZE"]) * 1024)
     trace = glob.glob(os.path.join(OUT, "pmc_clock", "**", "*kernel_trace.csv"), recursive=True)

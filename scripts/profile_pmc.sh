@@ -4,7 +4,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-ARGS="--no-cpu-baseline --no-alt --steps 2 --warmup 1 ${BENCH_ARGS}"
+ARGS="--no-cpu-baseline --no-alt --no-config-c --steps 2 --warmup 1 ${BENCH_ARGS}"
 run() {
   local name=$1; shift
   timeout -k 10 300 rocprofv3 --pmc "$@" --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_$name" -o run \

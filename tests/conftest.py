@@ -63,3 +63,10 @@ def config_scene(rt2mod, tmp_path_factory):
             _scene_cache[name] = rt2mod.build_config_scene(name, str(tmp_path_factory.mktemp("scenes")))
         return _scene_cache[name]
     return get
+
+
+def require_variant(rt2mod, v):
+    """Skips the calling test when kernel variant v is not in the loaded build
+    (A/B experiment variants: make EXPERIMENTS=1, RT2_LIB=exp)."""
+    if not rt2mod.has_variant(v):
+        pytest.skip(f"variant {v} is an experiment variant (not in the product build)")

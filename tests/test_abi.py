@@ -40,7 +40,7 @@ def test_struct_layouts(rt2mod):
 
 def test_abi_version_and_errors(rt2mod):
     L = rt2mod.lib()
-    assert L.rt2_abi_version() == 3
+    assert L.rt2_abi_version() == 4 == rt2mod.ABI_VERSION
     sd = rt2mod.SceneData()
     try:
         sd.load_obj_folder("/nonexistent/folder")
@@ -63,3 +63,32 @@ def test_shard_rows(rt2mod):
                     assert list(ids) == sorted(ids)
                     rows.extend(ids)
                 assert sorted(rows) == list(range(H))
+
+
+def test_comm_argument_validation(rt2mod):
+    """Multi-GPU ABI: argument errors are reported before any HIP/RCCL call
+    (no GPU needed)."""
+    L = rt2mod.lib()
+    p = C.c_void_p()
+    uid = (C.c_uint8 * rt2mod.COMM_ID_BYTES)()
+    assert L.rt2_comm_init(uid, 2, 2, 0, C.byref(p)) < 0  # rank outside [0, nranks)
+    assert b"bad argument" in L.rt2_last_error()
+    assert L.rt2_comm_init(None, 1, 0, 0, C.byref(p)) < 0
+    assert L.rt2_comm_wrap(None, 0, C.byref(p)) < 0
+    assert L.rt2_comm_check(None) < 0
+    assert L.rt2_gather_slabs(None, None, 8, 8, rt2mod.shard(), 0, None, None) < 0
+    # max_rows smaller than the largest slab of the layout
+    assert L.rt2_unshard_slabs(C.c_void_p(16), 1, 8, 8, rt2mod.shard(1, 0, 2), C.c_void_p(16), None) < 0
+    assert b"bad argument" in L.rt2_last_error()
+    L.rt2_comm_destroy(None)  # no-op
+
+
+def test_experiment_variants_not_in_product_build(rt2mod):
+    """The product library carries only the automatically chosen kernels
+    (DESIGN.md §Kernels); A/B variants live in the EXPERIMENTS=1 build."""
+    if os.environ.get("RT2_LIB") == "exp":
+        return
+    for v in (0, 53, 67, 85, 86):
+        assert rt2mod.has_variant(v)
+    for v in (1, 22, 28, 40, 46, 64, 74, 84, 87):
+        assert not rt2mod.has_variant(v)

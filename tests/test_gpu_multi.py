@@ -1,0 +1,146 @@
+"""Multi-GPU path on one GPU (the 8-GPU run is the driver's).
+
+- Config D (scene B at 3840x2160, 64 rays x 16 frames, 8 bounces — the 8-GPU
+  configuration of BASELINE.json): rendered whole, with the per-frame planes
+  forced into 4-frame chunks (the chunking path of rt2_render), and as the 8
+  row-tile shards the bench uses, each slab rendered on its own; the slabs,
+  packed as an RCCL gather leaves them on the root ([rank][max_rows][W]) and
+  un-interleaved by rt2_unshard_slabs, must equal the whole image bit for bit;
+  2,048 spread pixels at full spp must equal the CPU oracle bit for bit.
+- The C-ABI communicator (rt2_comm_*, RCCL): a one-rank communicator's
+  rt2_render_host_gather and rt2_gather_slabs reproduce rt2_render_host.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from test_gpu_parity import assert_exact
+
+pytestmark = pytest.mark.gpu
+
+N_SHARDS = 8
+TILE = 1  # bench.py --tile-rows default
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    torch.cuda.set_device(0)
+    return torch
+
+
+def render_slab(rt2mod, torch, scene, u, frames, sh, rows_alloc=None):
+    """Renders a shard into a device accumulator and resolves it on the device;
+    returns the resolved slab (rows_alloc rows, zero padded) as a torch tensor."""
+    rows = rt2mod.shard_rows(u.height, sh)
+    acc = torch.zeros((rows_alloc or rows, u.width, 4), dtype=torch.float32, device="cuda")
+    res = torch.zeros_like(acc)
+    stream = torch.cuda.current_stream().cuda_stream
+    scene.render(u, 0, frames, sh, acc.data_ptr(), 0, stream)
+    rt2mod.resolve_rgba32f(acc.data_ptr(), rows * u.width, frames, res.data_ptr(), stream)
+    return res
+
+
+@pytest.fixture(scope="module")
+def config_d(rt2mod, config_scene, torch_cuda):
+    sd, spec = config_scene("D")
+    assert (spec.width, spec.height, spec.rays, spec.frames, spec.bounces) == (3840, 2160, 64, 16, 8)
+    u = rt2mod.offline_uniforms(spec.width, spec.height, spec.bounces, spec.rays, sd.num_triangles)
+    scene = rt2mod.Scene(sd, 0)
+    L = rt2mod.lib()
+    L.rt2_scene_set_frame_scratch_cap.argtypes = [C.c_void_p, C.c_ulonglong]
+    plane = spec.width * spec.height * 16
+    assert L.rt2_scene_set_frame_scratch_cap(scene._p, 4 * plane) == 0  # 4-frame chunks
+    whole = render_slab(rt2mod, torch_cuda, scene, u, spec.frames, rt2mod.shard())
+    torch_cuda.cuda.synchronize()
+    st = scene.stats(reset=True)
+    assert st.samples == spec.width * spec.height * spec.rays * spec.frames
+    return sd, spec, u, whole
+
+
+def test_config_D_pixels_match_oracle(rt2mod, oraclemod, config_d):
+    """2,048 pixels spread over the 4K image, all 1,024 samples each, bit-exact."""
+    sd, spec, u, whole = config_d
+    img = whole.cpu().numpy()
+    n = 2048
+    pid = (np.arange(n, dtype=np.int64) * (spec.width * spec.height)) // n + 977  # off the row starts
+    xs, ys = pid % spec.width, pid // spec.width
+    acc, _, _, _ = oraclemod.render_pixels(sd.triangles(), sd.materials(), u, xs, ys, 0, spec.frames, "brute")
+    assert_exact(img[ys, xs], acc[:, :3] / np.float32(spec.frames), "config D sampled pixels")
+
+
+def test_config_D_eight_row_tile_shards_assemble(rt2mod, config_d, torch_cuda):
+    """The 8 rank slabs (1/8 of the rows each, no frame chunking: 265 MB of
+    planes per slab), gathered-layout + rt2_unshard_slabs == the whole image."""
+    torch = torch_cuda
+    sd, spec, u, whole = config_d
+    scene = rt2mod.Scene(sd, 0)
+    mr = max(rt2mod.shard_rows(spec.height, rt2mod.shard(TILE, r, N_SHARDS)) for r in range(N_SHARDS))
+    gathered = torch.zeros((N_SHARDS, mr, spec.width, 4), dtype=torch.float32, device="cuda")
+    for r in range(N_SHARDS):
+        sh = rt2mod.shard(TILE, r, N_SHARDS)
+        gathered[r] = render_slab(rt2mod, torch, scene, u, spec.frames, sh, rows_alloc=mr)
+    image = torch.empty_like(whole)
+    rt2mod.unshard_slabs(gathered.data_ptr(), mr, spec.width, spec.height, rt2mod.shard(TILE, 0, N_SHARDS),
+                         image.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    diff = (image != whole).any(-1)
+    assert not bool(diff.any()), f"{int(diff.sum())} pixels of the assembled shards differ from the whole render"
+
+
+def test_unshard_uneven_slabs(rt2mod, config_scene, torch_cuda):
+    """Ragged layouts: slabs of different heights (50 rows, tiles of 4 over 3
+    ranks), padded to max_rows as the gather leaves them."""
+    torch = torch_cuda
+    sd, spec = config_scene("B")
+    W, H, n, tile = 72, 50, 3, 4
+    u = rt2mod.offline_uniforms(W, H, spec.bounces, 2, sd.num_triangles)
+    scene = rt2mod.Scene(sd, 0)
+    whole = render_slab(rt2mod, torch, scene, u, 2, rt2mod.shard())
+    rows = [rt2mod.shard_rows(H, rt2mod.shard(tile, r, n)) for r in range(n)]
+    assert len(set(rows)) > 1
+    mr = max(rows)
+    gathered = torch.full((n, mr, W, 4), -1.0, dtype=torch.float32, device="cuda")
+    for r in range(n):
+        gathered[r] = render_slab(rt2mod, torch, scene, u, 2, rt2mod.shard(tile, r, n), rows_alloc=mr)
+    image = torch.zeros_like(whole)
+    rt2mod.unshard_slabs(gathered.data_ptr(), mr, W, H, rt2mod.shard(tile, 0, n), image.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(image, whole)
+
+
+def test_comm_one_rank_render_host_gather(rt2mod, config_scene, torch_cuda):
+    """rt2_render_host_gather over a one-rank RCCL communicator == rt2_render_host
+    (float mean and the 8-bit reference average)."""
+    sd, spec = config_scene("B")
+    W, H = 96, 54
+    u = rt2mod.offline_uniforms(W, H, spec.bounces, 4, sd.num_triangles)
+    scene = rt2mod.Scene(sd, 0)
+    ref, ref8 = scene.render_host(u, 2, 3, rgb8=True)
+    comm = rt2mod.Comm(rt2mod.Comm.unique_id(), 1, 0, 0)
+    for tile in (1, 5):
+        img, img8 = scene.render_host_gather(u, 2, 3, rt2mod.shard(tile, 0, 1), comm, 0, rgb8=True)
+        assert np.array_equal(img, ref) and np.array_equal(img8, ref8)
+    comm.check()
+    with pytest.raises(rt2mod.RT2Error):  # a shard of another communicator size
+        scene.render_host_gather(u, 0, 1, rt2mod.shard(1, 0, 2), comm, 0)
+    comm.close()
+
+
+def test_comm_gather_slabs_one_rank(rt2mod, config_scene, torch_cuda):
+    torch = torch_cuda
+    sd, spec = config_scene("B")
+    W, H = 64, 30
+    u = rt2mod.offline_uniforms(W, H, spec.bounces, 2, sd.num_triangles)
+    scene = rt2mod.Scene(sd, 0)
+    slab = render_slab(rt2mod, torch, scene, u, 1, rt2mod.shard())
+    image = torch.zeros_like(slab)
+    comm = rt2mod.Comm(rt2mod.Comm.unique_id(), 1, 0, 0)
+    comm.gather_slabs(slab.data_ptr(), W, H, rt2mod.shard(), 0, image.data_ptr(),
+                      torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    comm.check()
+    assert torch.equal(image, slab)
+    comm.close()

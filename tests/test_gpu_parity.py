@@ -11,6 +11,8 @@ import os
 import numpy as np
 import pytest
 
+from conftest import require_variant
+
 pytestmark = pytest.mark.gpu
 
 RMSE_TOL = 1e-4
@@ -223,7 +225,7 @@ def test_tiled_kernel_exact(rt2mod, oraclemod, config_scene, torch_cuda):
     sd, spec = config_scene("B")
     u = rt2mod.offline_uniforms(96, 54, 8, 4, sd.num_triangles)
     scene = rt2mod.Scene(sd, 0)
-    scene.set_variant(2)
+    scene.set_variant(86)
     img = scene.render_host(u, 0, 1)
     ref, _, segs = oracle_mean(oraclemod, sd, u, np.arange(54), 0, 1)
     assert_exact(img, ref, "tiled B")
@@ -288,9 +290,10 @@ def test_frame_split_identical(rt2mod, oraclemod, config_scene, torch_cuda, trav
 
 
 # brute-force kernel variants that change the schedule, not the arithmetic:
-# masked/ballot/min-filter sweeps, cooperative and team tail modes, occupancy hints
-BRUTE_VARIANTS = [0, 1, 2, 22, 24, 28, 31, 52, 59, 60, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73,
-                  74, 75, 76, 77, 78, 79, 80, 83, 84, 85, 86, 87, 88, 89]
+# the product variants (0, 67, 85, 86) and, in an experiment build, the A/B
+# variants (masked/plk filters, resident LDS, cooperative and team tail modes,
+# split waves, occupancy hints)
+BRUTE_VARIANTS = [0, 67, 85, 86, 22, 24, 28, 52, 64, 65, 66, 68, 70, 71, 72, 73, 74, 76, 79, 80, 84, 87, 89]
 PLK_VARIANTS = [74, 76, 79, 80]
 
 
@@ -303,6 +306,7 @@ def plk_info(rt2mod, scene):
 
 @pytest.mark.parametrize("variant", BRUTE_VARIANTS)
 def test_brute_variants_bit_exact(rt2mod, oraclemod, config_scene, torch_cuda, variant):
+    require_variant(rt2mod, variant)
     sd, spec = config_scene("B")
     W, H, R = 96, 54, 4
     u = rt2mod.offline_uniforms(W, H, spec.bounces, R, sd.num_triangles)
@@ -319,6 +323,7 @@ def test_brute_variants_bit_exact(rt2mod, oraclemod, config_scene, torch_cuda, v
 def test_plk_filter_diverse_materials(rt2mod, oraclemod, torch_cuda, variant):
     """Per-ray precomputed filter (sweep_plk) on glass/mirror/checker/glossy
     paths: every direction a path makes passes the per-segment range check."""
+    require_variant(rt2mod, variant)
     M = rt2mod.Material
     sd = rt2mod.SceneData()
     red = sd.add_material(M.diffuse((1, 0, 0)))
@@ -357,6 +362,7 @@ def test_plk_out_of_range_triangles(rt2mod, oraclemod, config_scene, torch_cuda)
     < 2^-30, a component below 2^-100, degenerate) get always-pass records and
     are decided by the exact test; with more than 1/64 of them the scene keeps
     the exact-intermediate filter.  Both renders match the oracle bit for bit."""
+    require_variant(rt2mod, 76)
     sd, spec = config_scene("B")
     extra = [((3e6, 0, -3e6), (3e6, 1, -3e6), (3e6, 0, -3e6 + 1)),        # |a| > 2^20
              ((0.1, 2.0, 3.0), (0.1 + 1e-10, 2.0, 3.0), (0.1, 2.0 + 1e-10, 3.0)),  # microscopic
@@ -376,12 +382,13 @@ def test_plk_out_of_range_triangles(rt2mod, oraclemod, config_scene, torch_cuda)
         assert_exact(img, ref, f"plk out-of-range x{n_copies}")
 
 
-@pytest.mark.parametrize("variant", [71, 72, 84])
+@pytest.mark.parametrize("variant", [85, 71, 72, 84])
 @pytest.mark.parametrize("split_frames", [False, True])
 def test_split_waves_outputs(rt2mod, oraclemod, config_scene, torch_cuda, variant, split_frames):
     """Split mode (S waves per 64 rays, one writer wave): the float and 8-bit
     accumulators, the per-frame planes and the counters see each pixel-frame
     once — identical to the default kernel on a shard slab with 3 frames."""
+    require_variant(rt2mod, variant)
     sd, spec = config_scene("B")
     W, H, R, F = 80, 45, 4, 3
     u = rt2mod.offline_uniforms(W, H, spec.bounces, R, sd.num_triangles)
@@ -406,6 +413,7 @@ def test_split_waves_outputs(rt2mod, oraclemod, config_scene, torch_cuda, varian
 def test_team_tail_small_slab(rt2mod, oraclemod, config_scene, torch_cuda, variant):
     """A slab smaller than the number of lanes (rank 5 of 8, tiles of 3 rows):
     the team mode runs from the first segment."""
+    require_variant(rt2mod, variant)
     sd, spec = config_scene("B")
     W, H = 160, 90
     u = rt2mod.offline_uniforms(W, H, spec.bounces, 8, sd.num_triangles)
