@@ -65,6 +65,12 @@ def config_scene(rt2mod, tmp_path_factory):
     return get
 
 
+# The experiment build (make EXPERIMENTS=1, RT2_LIB=exp) adds the A/B kernel
+# variants; their parity tests are collected only when it is loaded.
+EXPERIMENTS = os.environ.get("RT2_LIB") == "exp"
+collect_ignore = [] if EXPERIMENTS else ["test_gpu_experiments.py"]
+
+
 def require_variant(rt2mod, v):
     """Skips the calling test when kernel variant v is not in the loaded build
     (A/B experiment variants: make EXPERIMENTS=1, RT2_LIB=exp)."""

@@ -4,7 +4,7 @@ visiting-order tie behaviour, and equal leaf-test counts."""
 import numpy as np
 import pytest
 
-from conftest import require_variant
+from conftest import EXPERIMENTS, require_variant
 
 from test_gpu_parity import assert_exact, oracle_mean
 
@@ -95,7 +95,7 @@ def test_bvh_requires_nodes_and_validates(rt2mod, torch_cuda):
 # render_bvh2 (child-pair records, Markstein slabs, while-while) and
 # render_bvh3 (+ wave-uniform fast slab path, fused interior/leaf sub-steps)
 # (53 = the product kernel; the others are experiment-build variants)
-BVH2_VARIANTS = [53, 40, 41, 43, 45, 46, 47, 48, 50, 54, 55]
+BVH2_VARIANTS = [53] + ([40, 41, 43, 45, 46, 47, 48, 50, 54, 55] if EXPERIMENTS else [])
 BVH_SPOT = (53, 40, 46, 50, 55)
 
 
