@@ -437,7 +437,7 @@ constexpr int kTileTris = 1024;  // 48 KiB of LDS per tile
 // product build carries the variants the launcher chooses automatically; the
 // A/B experiments measured in DESIGN.md ("Tried and measured") are compiled
 // only with -DRT2_EXPERIMENTS (make EXPERIMENTS=1).
-enum Kind : int { K_RESIDENT = 0, K_TILED = 1, K_SMEM = 2, K_SPLIT = 3, K_BVH = 4, K_BVH2 = 5, K_BVH3 = 6 };
+enum Kind : int { K_RESIDENT = 0, K_TILED = 1, K_SMEM = 2, K_SPLIT = 3, K_ASSIST = 4, K_BVH = 5, K_BVH2 = 6, K_BVH3 = 7 };
 struct Variant {
     int id;
     int kind;
@@ -458,10 +458,14 @@ hipError_t launch_k(const RenderParams& p, int blocks, size_t lds, hipStream_t s
 // product kernels
 constexpr SmemSpec kSmemDefault{.block = 256, .group = 8, .filter = Filter::Max3, .tail = Tail::Coop,
                                 .tail_lanes = 32, .waves = 6, .stats = false};
+#ifdef RT2_EXPERIMENTS
 constexpr SmemSpec kSmemMid{.block = 256, .group = 8, .filter = Filter::Max3, .tail = Tail::Coop, .tail_lanes = 32,
                             .waves = 1, .stats = false};
 constexpr SplitSpec kSplitSmall{.waves_per_ray = 4, .group = 8, .filter = Filter::Max3, .waves = 6};
+constexpr AssistSpec kAssist8{.waves_per_block = 8, .group = 8, .filter = Filter::Max3, .waves = 6, .coop_rays = 48};
+#endif
 constexpr TiledSpec kTiledLarge{.block = 512, .group = 4, .filter = Filter::Max3};
+constexpr AssistSpec kAssist12{.waves_per_block = 12, .group = 8, .filter = Filter::Max3, .waves = 6, .coop_rays = 48};
 constexpr Bvh3Spec kBvhDefault{.block = 256, .thresh = 16, .slab = Slab::Markstein, .waves = 5, .diag = false};
 
 #ifdef RT2_EXPERIMENTS
@@ -479,10 +483,12 @@ constexpr Bvh3Spec bvh3_x(int t, Slab sl, int w, bool diag = false) {
 const Variant kVariants[] = {
     RT2_VARIANT(0, K_SMEM, render_smem<kSmemDefault>, 256, "smem/256/max3f8/coop32/w6"),  // default (<= kSmemMaxTris)
     RT2_VARIANT(53, K_BVH3, render_bvh3<kBvhDefault>, 256, "bvh3/256/t16/w5"),            // default (BVH traversal)
-    RT2_VARIANT(67, K_SMEM, render_smem<kSmemMid>, 256, "smem/256/max3f8/coop32"),         // 1-4 items per lane
-    RT2_VARIANT(85, K_SPLIT, render_split<kSplitSmall>, 256, "split4/max3f8/w6"),          // < 1 item per lane
     RT2_VARIANT(86, K_TILED, render_tiled<kTiledLarge>, 512, "tiled/512/max3f4"),          // > kSmemMaxTris
+    RT2_VARIANT(92, K_ASSIST, render_assist<kAssist12>, 768, "assist12/max3f8/w6"),        // < 4 items per lane
 #ifdef RT2_EXPERIMENTS
+    RT2_VARIANT(67, K_SMEM, render_smem<kSmemMid>, 256, "smem/256/max3f8/coop32"),         // round-1 choice, 1-4 items per lane
+    RT2_VARIANT(85, K_SPLIT, render_split<kSplitSmall>, 256, "split4/max3f8/w6"),          // round-1 choice, < 1 item per lane
+    RT2_VARIANT(90, K_ASSIST, render_assist<kAssist8>, 512, "assist8/max3f8/w6"),
     RT2_VARIANT(22, K_RESIDENT, (render_resident<ResidentSpec{512, 8, Filter::Five}>), 512, "resident/512/masked8"),
     RT2_VARIANT(24, K_SMEM, render_smem<smem_x(8, Filter::Five, Tail::None, 0, 1)>, 256, "smem/256/masked8"),
     RT2_VARIANT(26, K_TILED, (render_tiled<TiledSpec{512, 4, Filter::Five}>), 512, "tiled/512/masked4"),
@@ -528,9 +534,8 @@ constexpr size_t kResidentMaxBytes = 112 * 1024;
 constexpr int kSmemMaxTris = 131072;  // scalar path up to 6.3 MB of records (config C: 781 vs 817 ms tiled; config E: tiled 1,704 vs 2,312 ms)
 constexpr int kDefaultBrute = 0;
 constexpr int kDefaultBvh = 53;
-constexpr int kSmallSlab = 85;   // split4/max3f8/w6: brute force on slabs with fewer items than lanes
 constexpr int kLargeScene = 86;  // tiled/512/max3f4: LDS tiles above kSmemMaxTris triangles
-constexpr int kMidSlab = 67;     // smem/256/max3f8/coop32 (5 waves/SIMD): 1 to 4 items per lane
+constexpr int kSlab = 92;        // assist12/max3f8/w6: fewer than 4 items per lane (multi-GPU slabs)
 
 const Variant* find_variant(int id) {
     for (const Variant& v : kVariants)
@@ -752,27 +757,18 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     if (!VP) {
         int vi = s->n_tris <= kSmemMaxTris ? kDefaultBrute : kLargeScene;
         if (vi == kDefaultBrute) {
-            // items per resident lane decide the tail: a lane ends on a
-            // whole item, so with few items per lane the last round runs
-            // partly empty.  >= 4 per lane at 6 waves/SIMD (a full config B
-            // image): the 6-wave kernel; fewer: the 5-wave kernel (1/2 and
-            // 1/4 slabs: 3-4 % faster than 6 waves there); fewer items than
-            // 5-wave lanes (a 1/8 slab: 259k pixels, 327k lanes): every lane
-            // owns at most one long item, so the split-wave kernel traces
-            // each 64 rays with S waves (1/S of the triangles each)
-            auto lanes = [&](int v, unsigned long long& out) -> int {
-                const Variant* W = find_variant(v);
-                int occ0 = 0;
-                HIPCHECK(variant_occupancy(*W, &occ0, 0));
-                out = (unsigned long long)s->num_cus * (unsigned long long)std::max(occ0, 1) * W->block;
-                return 0;
-            };
-            unsigned long long lanes6 = 0, lanes5 = 0;
-            if (lanes(kDefaultBrute, lanes6) < 0 || lanes(kMidSlab, lanes5) < 0) return -1;
-            if (p.n_items < lanes5)
-                vi = kSmallSlab;
-            else if (p.n_items < 4 * lanes6)
-                vi = kMidSlab;
+            // items per resident lane decide the tail: a lane ends on a whole
+            // item (a pixel-frame's rays share one RNG stream), so with few
+            // items per lane the last round runs partly empty.  At >= 4 per
+            // lane (a full config B image) the 6-wave scalar-path kernel; below
+            // (the 1/2, 1/4, 1/8 slabs of config B on 2, 4, 8 GPUs) the assist
+            // kernel, whose idle waves sweep triangle chunks of the busy
+            // waves' rays
+            const Variant* W = find_variant(kSlab);
+            int occ0 = 0;
+            HIPCHECK(variant_occupancy(*W, &occ0, 0));
+            const unsigned long long lanes = (unsigned long long)s->num_cus * (unsigned long long)std::max(occ0, 1) * W->block;
+            if (p.n_items < 4 * lanes) vi = kSlab;
         }
         VP = find_variant(vi);
     }
@@ -792,8 +788,24 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     HIPCHECK(variant_occupancy(V, &occ, lds));
     occ = std::max(occ, 1);
     unsigned long long blocks = (unsigned long long)s->num_cus * occ;
-    const int rays_per_block = V.kind == K_SPLIT ? 64 : V.block;  // split: S waves per 64 rays
-    blocks = std::min(blocks, (p.n_items + rays_per_block - 1) / rays_per_block);
+    if (V.kind == K_ASSIST) {
+        // every resident workgroup is launched: waves without items help the
+        // busy waves of their workgroup.  Below 2 items per lane a quarter of
+        // the waves take items (each owner has ~3 helpers; 1/4 and 1/8 slabs
+        // of config B: 144 / 77 ms against 153 / 81 with half, 151 / 83 with
+        // all), otherwise all of them; a chunk job has ~2 chunks per wave.
+        const int nw = V.block / 64;
+        const unsigned long long lanes = blocks * (unsigned long long)V.block;
+        p.assist_cap = p.n_items < 2 * lanes ? std::max(1, nw / 4) : nw;
+        const int g = 8;  // the sweep's filter group
+        int chunk = (s->n_tris + 2 * nw - 1) / (2 * nw);
+        chunk = std::max(g, (chunk + g - 1) / g * g);
+        p.assist_chunk = chunk;
+        p.assist_nchunks = s->n_tris > 0 ? (s->n_tris + chunk - 1) / chunk : 0;  // <= 2 * nw
+    } else {
+        const int rays_per_block = V.kind == K_SPLIT ? 64 : V.block;  // split: S waves per 64 rays
+        blocks = std::min(blocks, (p.n_items + rays_per_block - 1) / rays_per_block);
+    }
     blocks = std::max(blocks, 1ull);
     s->last_variant = V.id;
     HIPCHECK(V.launch(p, (int)blocks, lds, st));

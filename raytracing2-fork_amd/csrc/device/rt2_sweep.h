@@ -59,6 +59,9 @@ struct RenderParams {
     int num_textures;            // uniforms.numTextures
     const float4* plk;           // nullable: per-ray-precomputed filter records (sweep_plk), 4 float4 each
     float plk_A;                 // max |a_i| over the scene's triangles (sweep_plk error bound)
+    int assist_cap;              // ASSIST: waves per workgroup that take items (the others start as helpers)
+    int assist_chunk;            // ASSIST: triangles per chunk of a posted sweep (a multiple of the group)
+    int assist_nchunks;          // ASSIST: chunks per sweep (< 4096)
 };
 
 enum : int { ST_NEED_ITEM = 0, ST_NEW_FRAME = 1, ST_NEW_RAY = 2, ST_TRACE = 3, ST_DONE = 4 };

@@ -19,6 +19,7 @@ ap.add_argument("--traversal", default="brute")
 ap.add_argument("--tile-rows", type=int, default=1)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--variants", default="0")
+ap.add_argument("--ns", default="1,2,4,8", help="slab counts N to time (1/N of the image each)")
 ap.add_argument("--cost-order", type=int, default=-1, help="1/0: most-expensive-first item order on/off")
 a = ap.parse_args()
 sd, spec = rt2.build_config_scene(a.config)
@@ -29,11 +30,16 @@ if a.cost_order >= 0:
     scene.set_cost_order(bool(a.cost_order))
 
 
+first = {}  # slab image of the first variant, per N: every variant must match it bit for bit
+
+
 def slab_time(sh):
     rows = rt2.shard_rows(spec.height, sh)
     acc = torch.zeros((rows, spec.width, 4), device="cuda")
     scene.render(u, 0, spec.frames, sh, acc.data_ptr())
     torch.cuda.synchronize()
+    ref = first.setdefault(sh.nranks, acc.clone())
+    assert torch.equal(acc, ref), f"slab 1/{sh.nranks} differs from the first variant's"
     ts = []
     for _ in range(a.reps):
         acc.zero_()
@@ -47,9 +53,9 @@ def slab_time(sh):
 
 for var in [int(v) for v in a.variants.split(",")]:
     scene.set_variant(var)
-    out = {n: slab_time(rt2.shard(a.tile_rows, 0, n)) for n in (1, 2, 4, 8)}
-    base = out[1]
+    out = {n: slab_time(rt2.shard(a.tile_rows, 0, n)) for n in [int(x) for x in a.ns.split(",")]}
+    base = out.get(1)
     print(json.dumps({"config": a.config, "traversal": a.traversal, "tile_rows": a.tile_rows, "variant": var, "cost_order": a.cost_order,
                       "name": rt2.lib().rt2_variant_name(var).decode() if var else "auto",
                       "slab_ms": {n: round(t * 1e3, 2) for n, t in out.items()},
-                      "predicted_efficiency": {n: round(base / n / t, 3) for n, t in out.items()}}), flush=True)
+                      "predicted_efficiency": {n: round(base / n / t, 3) for n, t in out.items()} if base else None}), flush=True)

@@ -102,15 +102,17 @@ def _last_variant(rt2mod, scene):
 
 def test_auto_variant_by_items_per_lane(rt2mod, config_scene, torch_cuda):
     """The launcher picks the brute kernel by items per resident lane (DESIGN.md
-    §Kernels): the 6-wave kernel for the full config B image, the 5-wave kernel
-    for a 1/2 slab, the split-wave kernel for a 1/8 slab — and every slab is
-    bit-identical to the same rows of the full image."""
+    §Kernels): the 6-wave scalar-path kernel for the full config B image, the
+    assist kernel (idle waves sweep chunks of the busy waves' rays) for the
+    1/2, 1/4 and 1/8 slabs — all waves owning items at 1/2, a quarter of them
+    below 2 items per lane — and every slab is bit-identical to the same rows
+    of the full image."""
     sd, spec = config_scene("B")
     u = rt2mod.offline_uniforms(spec.width, spec.height, spec.bounces, spec.rays, sd.num_triangles)
     scene = rt2mod.Scene(sd, 0)
     full = scene.render_host(u, 0, 1)
     assert _last_variant(rt2mod, scene) == "smem/256/max3f8/coop32/w6"
-    for n, want in ((2, "smem/256/max3f8/coop32"), (8, "split4/max3f8/w6")):
+    for n, want in ((2, "assist12/max3f8/w6"), (4, "assist12/max3f8/w6"), (8, "assist12/max3f8/w6")):
         sh = rt2mod.shard(1, n - 1, n)
         img = scene.render_host(u, 0, 1, sh)
         assert _last_variant(rt2mod, scene) == want
@@ -290,11 +292,11 @@ def test_frame_split_identical(rt2mod, oraclemod, config_scene, torch_cuda, trav
 
 
 # brute-force kernel variants that change the schedule, not the arithmetic:
-# the product variants (0, 67, 85, 86) and, in an experiment build, the A/B
+# the product variants (0, 86, 92) and, in an experiment build, the A/B
 # variants (masked/plk filters, resident LDS, cooperative and team tail modes,
-# split waves, occupancy hints)
-BRUTE_VARIANTS = [0, 67, 85, 86] + ([22, 24, 28, 52, 64, 65, 66, 68, 70, 71, 72, 73, 74, 76, 79, 80, 84, 87, 89]
-                                    if EXPERIMENTS else [])
+# split waves, the round-1 slab kernels, occupancy hints)
+BRUTE_VARIANTS = [0, 86, 92] + ([22, 24, 28, 52, 64, 65, 66, 67, 68, 70, 71, 72, 73, 74, 76, 79, 80, 84, 85, 87, 89,
+                                 90] if EXPERIMENTS else [])
 
 
 @pytest.mark.parametrize("variant", BRUTE_VARIANTS)
@@ -312,12 +314,14 @@ def test_brute_variants_bit_exact(rt2mod, oraclemod, config_scene, torch_cuda, v
     assert st.segments == segs
 
 
-@pytest.mark.parametrize("variant", [85] + ([71, 72, 84] if EXPERIMENTS else []))
+@pytest.mark.parametrize("variant", [92] + ([71, 72, 84, 85, 90] if EXPERIMENTS else []))
 @pytest.mark.parametrize("split_frames", [False, True])
 def test_split_waves_outputs(rt2mod, oraclemod, config_scene, torch_cuda, variant, split_frames):
-    """Split mode (S waves per 64 rays, one writer wave): the float and 8-bit
-    accumulators, the per-frame planes and the counters see each pixel-frame
-    once — identical to the default kernel on a shard slab with 3 frames."""
+    """Kernels whose waves share rays — split mode (S waves per 64 rays, one
+    writer wave) and the assist kernel (helpers sweep chunks or whole rays of
+    an owner's segment): the float and 8-bit accumulators, the per-frame planes
+    and the counters see each pixel-frame once — identical to the default
+    kernel on a shard slab with 3 frames."""
     require_variant(rt2mod, variant)
     sd, spec = config_scene("B")
     W, H, R, F = 80, 45, 4, 3
