@@ -259,7 +259,7 @@ struct AssistSpec {
     int group;
     Filter filter;
     int waves;       // minimum waves per SIMD the register allocation must allow
-    int coop_rays;   // ray jobs for at most this many live rays (chunk jobs above)
+    int coop_rays;   // with helpers: ray jobs for at most this many live rays (chunk jobs above)
 };
 
 template <int NW>
@@ -374,14 +374,18 @@ __global__ __launch_bounds__(64 * S.waves_per_block) __attribute__((amdgpu_waves
     Lane L;
     lane_init(L);
     uint32_t seq = 0;
+    unsigned long long t_start = 0, t_dry = 0;  // wave_log diagnostic
+    if (p.wave_log) t_start = __builtin_amdgcn_s_memrealtime();
     if (w < cap) {
         for (;;) {
             advance(L, p);
             const unsigned long long act = __ballot(L.st == ST_TRACE);
+            if (p.wave_log && !t_dry && __any(L.st == ST_DONE)) t_dry = __builtin_amdgcn_s_memrealtime();
             if (!act) break;
             const uint32_t live = (uint32_t)__popcll(act);
             const bool helped = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&sh.helpers, __ATOMIC_RELAXED, WG)) > 0;
-            const bool ray_job = live <= (uint32_t)S.coop_rays && (helped || (live <= 32u && __any(L.st == ST_DONE)));
+            // without helpers: SMEM's cooperative drain (<= 32 live rays, pool dry)
+            const bool ray_job = helped ? live <= (uint32_t)S.coop_rays : live <= 32u && __any(L.st == ST_DONE);
             const bool chunk_job = !ray_job && helped && p.assist_nchunks > 1;
             float best = 1e38f, bestK = 1e38f * 1.0009765625f;
             int bi = -1;
@@ -424,6 +428,18 @@ __global__ __launch_bounds__(64 * S.waves_per_block) __attribute__((amdgpu_waves
     if (lane == 0) __hip_atomic_fetch_add(&sh.helpers, 1, __ATOMIC_RELAXED, WG);
     assist_work<S, NW>(p, sh, w, -1, 0);
     flush_counters(L, p);
+    if (p.wave_log) {
+        const uint32_t gw = blockIdx.x * NW + (uint32_t)w;
+        unsigned long long sg = L.segs;
+        for (int off = 32; off > 0; off >>= 1) sg += __shfl_xor(sg, off);
+        if (lane == 0 && gw < p.wave_log_n) {
+            unsigned long long* e = p.wave_log + 4 * (size_t)gw;
+            e[0] = t_start;
+            e[1] = t_dry;
+            e[2] = __builtin_amdgcn_s_memrealtime();
+            e[3] = sg;
+        }
+    }
 }
 
 }  // namespace

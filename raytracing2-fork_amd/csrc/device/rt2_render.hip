@@ -104,6 +104,8 @@ struct rt2_scene {
     uint4* d_host_acc8 = nullptr;   // 8-bit path sums
     uint8_t* d_host_rgb8 = nullptr; // 8-bit path result (3 B per pixel)
     size_t host_cap = 0;            // pixels the four buffers hold
+    unsigned long long* wave_log = nullptr;  // diagnostic wave timeline (rt2_scene_set_wave_log)
+    uint32_t wave_log_n = 0;
 };
 
 // Validates a reference node array (BVH.h layout) against the triangle count
@@ -264,6 +266,16 @@ extern "C" int rt2_scene_set_cost_order(rt2_scene* s, int enable) {
     }
     s->cost_order = enable ? 1 : 0;
     s->cost_npix = 0;  // forget the map
+    return 0;
+}
+
+// Not in rt2.h (diagnostics): the assist kernel writes a per-wave timeline
+// {start, first item-less lane, end, segments} in 10-ns ticks to d_log
+// (4 x u64 per wave, n waves; null turns it off).
+extern "C" int rt2_scene_set_wave_log(rt2_scene* s, unsigned long long* d_log, uint32_t n) {
+    if (!s) return -1;
+    s->wave_log = d_log;
+    s->wave_log_n = d_log ? n : 0;
     return 0;
 }
 
@@ -462,10 +474,13 @@ constexpr SmemSpec kSmemDefault{.block = 256, .group = 8, .filter = Filter::Max3
 constexpr SmemSpec kSmemMid{.block = 256, .group = 8, .filter = Filter::Max3, .tail = Tail::Coop, .tail_lanes = 32,
                             .waves = 1, .stats = false};
 constexpr SplitSpec kSplitSmall{.waves_per_ray = 4, .group = 8, .filter = Filter::Max3, .waves = 6};
-constexpr AssistSpec kAssist8{.waves_per_block = 8, .group = 8, .filter = Filter::Max3, .waves = 6, .coop_rays = 48};
+constexpr AssistSpec kAssist8{.waves_per_block = 8, .group = 8, .filter = Filter::Max3, .waves = 6, .coop_rays = 32};
+constexpr AssistSpec assist12_x(int coop) {
+    return AssistSpec{.waves_per_block = 12, .group = 8, .filter = Filter::Max3, .waves = 6, .coop_rays = coop};
+}
 #endif
 constexpr TiledSpec kTiledLarge{.block = 512, .group = 4, .filter = Filter::Max3};
-constexpr AssistSpec kAssist12{.waves_per_block = 12, .group = 8, .filter = Filter::Max3, .waves = 6, .coop_rays = 48};
+constexpr AssistSpec kAssist12{.waves_per_block = 12, .group = 8, .filter = Filter::Max3, .waves = 6, .coop_rays = 32};
 constexpr Bvh3Spec kBvhDefault{.block = 256, .thresh = 16, .slab = Slab::Markstein, .waves = 5, .diag = false};
 
 #ifdef RT2_EXPERIMENTS
@@ -489,6 +504,8 @@ const Variant kVariants[] = {
     RT2_VARIANT(67, K_SMEM, render_smem<kSmemMid>, 256, "smem/256/max3f8/coop32"),         // round-1 choice, 1-4 items per lane
     RT2_VARIANT(85, K_SPLIT, render_split<kSplitSmall>, 256, "split4/max3f8/w6"),          // round-1 choice, < 1 item per lane
     RT2_VARIANT(90, K_ASSIST, render_assist<kAssist8>, 512, "assist8/max3f8/w6"),
+    RT2_VARIANT(95, K_ASSIST, render_assist<assist12_x(48)>, 768, "assist12/max3f8/w6/coop48"),
+    RT2_VARIANT(97, K_ASSIST, render_assist<assist12_x(16)>, 768, "assist12/max3f8/w6/coop16"),
     RT2_VARIANT(22, K_RESIDENT, (render_resident<ResidentSpec{512, 8, Filter::Five}>), 512, "resident/512/masked8"),
     RT2_VARIANT(24, K_SMEM, render_smem<smem_x(8, Filter::Five, Tail::None, 0, 1)>, 256, "smem/256/masked8"),
     RT2_VARIANT(26, K_TILED, (render_tiled<TiledSpec{512, 4, Filter::Five}>), 512, "tiled/512/masked4"),
@@ -664,6 +681,8 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     p.item_counter = s->d_counters;
     p.seg_counter = s->d_counters + 1;
     p.tile_tris = kTileTris;
+    p.wave_log = s->wave_log;
+    p.wave_log_n = s->wave_log_n;
 
     // renders of one scene share its counters and scratch (frame planes, cost
     // map, pixel order): a render waits for the scene's previous one, whatever

@@ -62,6 +62,8 @@ struct RenderParams {
     int assist_cap;              // ASSIST: waves per workgroup that take items (the others start as helpers)
     int assist_chunk;            // ASSIST: triangles per chunk of a posted sweep (a multiple of the group)
     int assist_nchunks;          // ASSIST: chunks per sweep (< 4096)
+    unsigned long long* wave_log;  // nullable diagnostic: per wave {start, pool dry, end, segments} (ASSIST)
+    uint32_t wave_log_n;           // waves the log holds
 };
 
 enum : int { ST_NEED_ITEM = 0, ST_NEW_FRAME = 1, ST_NEW_RAY = 2, ST_TRACE = 3, ST_DONE = 4 };
