@@ -71,15 +71,21 @@ def parse():
     return ap.parse_args()
 
 
-def kernel_source_digest():
-    """sha256 over the device sources compiled into the render kernels; a PMC
-    profile carries the digest of the sources it was measured on."""
+# Device sources the brute-force and BVH render kernels are compiled from (one
+# translation unit; the launcher policy in rt2_render.hip does not change their
+# code).  A PMC profile carries the digest of the sources it was measured on.
+KERNEL_SOURCES = ["raytracing2-fork_amd/csrc/device/rt2_math.h", "raytracing2-fork_amd/csrc/device/rt2_sweep.h",
+                  "raytracing2-fork_amd/csrc/device/rt2_path.h", "include/rt2_pinned_math.h", "include/rt2.h"]
+KERNEL_SOURCES_BY_TRAVERSAL = {"brute": ["raytracing2-fork_amd/csrc/device/rt2_brute.h"],  # the 1-GPU kernels
+                               "bvh": ["raytracing2-fork_amd/csrc/device/rt2_bvh.h"]}
+
+
+def kernel_source_digest(traversal="brute"):
+    """sha256 over the sources of one traversal's kernels."""
     h = hashlib.sha256()
-    files = sorted(glob.glob(os.path.join(ROOT, "raytracing2-fork_amd", "csrc", "device", "*")))
-    files.append(os.path.join(ROOT, "include", "rt2_pinned_math.h"))
-    for f in files:
+    for f in KERNEL_SOURCES + KERNEL_SOURCES_BY_TRAVERSAL[traversal]:
         h.update(os.path.basename(f).encode())
-        with open(f, "rb") as fh:
+        with open(os.path.join(ROOT, f), "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()
 
@@ -126,7 +132,7 @@ def attach_traffic(rf, config, variant, kern_ms):
         return
     with open(path) as f:
         prof = json.load(f)
-    digest = kernel_source_digest()
+    digest = kernel_source_digest("bvh" if config.endswith("_bvh") else "brute")
     if prof.get("kernel_variant") != variant or prof.get("kernel_source_sha256") != digest:
         rf["traffic_note"] = (f"profiles/pmc_config{config}.json was measured on variant "
                               f"{prof.get('kernel_variant')} / sources {str(prof.get('kernel_source_sha256'))[:12]}, "

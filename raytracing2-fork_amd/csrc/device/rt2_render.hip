@@ -35,6 +35,7 @@ using namespace rt2d;
 #include "rt2_sweep.h"
 #include "rt2_path.h"
 #include "rt2_brute.h"
+#include "rt2_assist.h"
 #include "rt2_bvh.h"
 #include "rt2_misc_kernels.h"
 

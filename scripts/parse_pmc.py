@@ -49,7 +49,7 @@ def main(config="B"):
     for name in ("fetch", "write", "valu", "salu", "clock", "wait"):
         res.update(load(name))
     out = {"config": config, "kernel_variant": bench_variant("fetch"),
-           "kernel_source_sha256": kernel_source_digest(), "counters_per_launch": res}
+           "kernel_source_sha256": kernel_source_digest("bvh" if config.endswith("_bvh") else "brute"), "counters_per_launch": res}
     if "FETCH_SIZE" in res and "WRITE_SIZE" in res:
         out["hbm_bytes_per_launch"] = int((2 * res["FETCH_SIZE"] + res["WRITE_SIZE"]) * 1024)
     trace = glob.glob(os.path.join(OUT, "pmc_clock", "**", "*kernel_trace.csv"), recursive=True)
