@@ -37,6 +37,7 @@ import glob
 import hashlib
 import json
 import os
+import re
 import sys
 import time
 
@@ -80,13 +81,21 @@ KERNEL_SOURCES_BY_TRAVERSAL = {"brute": ["raytracing2-fork_amd/csrc/device/rt2_b
                                "bvh": ["raytracing2-fork_amd/csrc/device/rt2_bvh.h"]}
 
 
+def _code_only(text):
+    """Source text without comments and blank-line differences (a comment edit
+    does not change the kernel)."""
+    text = re.sub(r"/\*.*?\*/", " ", text, flags=re.S)
+    text = re.sub(r"//[^\n]*", "", text)
+    return "\n".join(line.rstrip() for line in text.splitlines() if line.strip())
+
+
 def kernel_source_digest(traversal="brute"):
-    """sha256 over the sources of one traversal's kernels."""
+    """sha256 over the code (comments stripped) of one traversal's kernel sources."""
     h = hashlib.sha256()
     for f in KERNEL_SOURCES + KERNEL_SOURCES_BY_TRAVERSAL[traversal]:
         h.update(os.path.basename(f).encode())
-        with open(os.path.join(ROOT, f), "rb") as fh:
-            h.update(fh.read())
+        with open(os.path.join(ROOT, f), encoding="utf-8") as fh:
+            h.update(_code_only(fh.read()).encode())
     return h.hexdigest()
 
 

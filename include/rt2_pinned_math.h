@@ -12,7 +12,7 @@
  * use only IEEE-754 operations that are correctly rounded on both x86-64
  * (SSE/FMA) and gfx950 (v_fma_f32, v_mul/v_add, v_cvt), so the same code gives
  * the same bits on the host and on the device.  Accuracy (checked against the
- * system libm in tests/test_pinned_math.py) is within a few ulp, well inside
+ * system libm in tests/test_oracle_kat.py) is within a few ulp, well inside
  * GLSL's own allowance.
  *
  * This header is the product's own libm (like <math.h>), shared by the HIP

@@ -23,6 +23,7 @@ struct SmemSpec {
     int tail_lanes;  // the tail mode starts when at most this many lanes trace
     int waves;       // minimum waves per SIMD the register allocation must allow (1 = unconstrained)
     bool stats;      // diagnostic build: filter survivor counters
+    bool lockstep = false;  // one workgroup barrier per segment: the waves start their sweeps together
 };
 struct SplitSpec {
     int waves_per_ray;  // S: waves that trace the same 64 rays (1/S of the triangles each)
@@ -105,7 +106,10 @@ __global__ __launch_bounds__(S.block) void render_tiled(RenderParams p) {
 // SMEM: no LDS; triangles reach the VALU through the scalar cache.  With a
 // tail mode, once the item pool is exhausted (some lane is DONE) and at most
 // S.tail_lanes lanes of the wave still trace, the live rays' closest hits are
-// computed by several lanes each (coop_closest / team_closest).
+// computed by several lanes each (coop_closest / team_closest).  Lockstep:
+// the workgroup's waves start every segment's sweep together (one barrier per
+// segment), so the record lines one wave brings into the scalar cache serve
+// the others (config B: 521-523 vs 520-557 ms free-running, same bits).
 template <SmemSpec S>
 __device__ __forceinline__ void smem_body(const RenderParams& p) {
     FiltStats fs;
@@ -114,7 +118,12 @@ __device__ __forceinline__ void smem_body(const RenderParams& p) {
     for (;;) {
         advance(L, p);
         const unsigned long long act = __ballot(L.st == ST_TRACE);
-        if (!act) break;
+        if constexpr (S.lockstep) {
+            if (!__syncthreads_or(act != 0)) break;
+            if (!act) continue;
+        } else {
+            if (!act) break;
+        }
         if constexpr (S.tail == Tail::Team) {
             if (__popcll(act) <= (unsigned)S.tail_lanes && __any(L.st == ST_DONE)) {
                 float b;

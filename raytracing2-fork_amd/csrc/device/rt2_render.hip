@@ -470,12 +470,18 @@ hipError_t launch_k(const RenderParams& p, int blocks, size_t lds, hipStream_t s
 
 // product kernels
 constexpr SmemSpec kSmemDefault{.block = 256, .group = 8, .filter = Filter::Max3, .tail = Tail::Coop,
-                                .tail_lanes = 32, .waves = 6, .stats = false};
+                                .tail_lanes = 32, .waves = 6, .stats = false, .lockstep = true};
 #ifdef RT2_EXPERIMENTS
 constexpr SmemSpec kSmemMid{.block = 256, .group = 8, .filter = Filter::Max3, .tail = Tail::Coop, .tail_lanes = 32,
                             .waves = 1, .stats = false};
 constexpr SplitSpec kSplitSmall{.waves_per_ray = 4, .group = 8, .filter = Filter::Max3, .waves = 6};
 constexpr AssistSpec kAssist8{.waves_per_block = 8, .group = 8, .filter = Filter::Max3, .waves = 6, .coop_rays = 32};
+constexpr SmemSpec kSmemFree{.block = 256, .group = 8, .filter = Filter::Max3, .tail = Tail::Coop, .tail_lanes = 32,
+                             .waves = 6, .stats = false, .lockstep = false};
+constexpr SmemSpec kSmemLock128{.block = 128, .group = 8, .filter = Filter::Max3, .tail = Tail::Coop, .tail_lanes = 32,
+                                .waves = 6, .stats = false, .lockstep = true};
+constexpr SmemSpec kSmemLock512{.block = 512, .group = 8, .filter = Filter::Max3, .tail = Tail::Coop, .tail_lanes = 32,
+                                .waves = 6, .stats = false, .lockstep = true};
 constexpr AssistSpec assist12_x(int coop) {
     return AssistSpec{.waves_per_block = 12, .group = 8, .filter = Filter::Max3, .waves = 6, .coop_rays = coop};
 }
@@ -497,7 +503,7 @@ constexpr Bvh3Spec bvh3_x(int t, Slab sl, int w, bool diag = false) {
 #endif
 
 const Variant kVariants[] = {
-    RT2_VARIANT(0, K_SMEM, render_smem<kSmemDefault>, 256, "smem/256/max3f8/coop32/w6"),  // default (<= kSmemMaxTris)
+    RT2_VARIANT(0, K_SMEM, render_smem<kSmemDefault>, 256, "smem/256/max3f8/coop32/w6/lockstep"),  // default (<= kSmemMaxTris)
     RT2_VARIANT(53, K_BVH3, render_bvh3<kBvhDefault>, 256, "bvh3/256/t16/w5"),            // default (BVH traversal)
     RT2_VARIANT(86, K_TILED, render_tiled<kTiledLarge>, 512, "tiled/512/max3f4"),          // > kSmemMaxTris
     RT2_VARIANT(92, K_ASSIST, render_assist<kAssist12>, 768, "assist12/max3f8/w6"),        // < 4 items per lane
@@ -506,6 +512,9 @@ const Variant kVariants[] = {
     RT2_VARIANT(85, K_SPLIT, render_split<kSplitSmall>, 256, "split4/max3f8/w6"),          // round-1 choice, < 1 item per lane
     RT2_VARIANT(90, K_ASSIST, render_assist<kAssist8>, 512, "assist8/max3f8/w6"),
     RT2_VARIANT(95, K_ASSIST, render_assist<assist12_x(48)>, 768, "assist12/max3f8/w6/coop48"),
+    RT2_VARIANT(101, K_SMEM, render_smem<kSmemLock512>, 512, "smem/512/max3f8/coop32/w6/lockstep"),
+    RT2_VARIANT(104, K_SMEM, render_smem<kSmemLock128>, 128, "smem/128/max3f8/coop32/w6/lockstep"),
+    RT2_VARIANT(106, K_SMEM, render_smem<kSmemFree>, 256, "smem/256/max3f8/coop32/w6/free"),  // round-1 default
     RT2_VARIANT(97, K_ASSIST, render_assist<assist12_x(16)>, 768, "assist12/max3f8/w6/coop16"),
     RT2_VARIANT(22, K_RESIDENT, (render_resident<ResidentSpec{512, 8, Filter::Five}>), 512, "resident/512/masked8"),
     RT2_VARIANT(24, K_SMEM, render_smem<smem_x(8, Filter::Five, Tail::None, 0, 1)>, 256, "smem/256/masked8"),
