@@ -51,8 +51,9 @@ FLOP_PER_TEST = 53
 FLOP_PER_VISIT = 24        # BVH interior node: 2 boxes x (6 sub + 6 div), compute.glsl:382-408
 BYTES_PER_TEST = 36        # a, b, c positions
 TARGET_RATIO = 10.0        # north star: >= 10x the CPU reference at config C on 1 GPU
-KERNEL_FILES = {"smem": "render_smem", "split": "render_split", "tiled": "render_tiled",
-                "resident": "render_resident", "bvh3": "render_bvh3", "bvh2": "render_bvh2", "bvh": "render_bvh"}
+KERNEL_FILES = {"smem": "render_smem", "split": "render_split", "tiled": "render_tiled", "assist": "render_assist",
+                "resident": "render_resident", "bvh4": "render_bvh4", "bvh3": "render_bvh3", "bvh2": "render_bvh2",
+                "bvh": "render_bvh"}
 
 
 def parse():

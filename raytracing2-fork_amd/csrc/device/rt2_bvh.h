@@ -585,6 +585,152 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
     }
 }
 
+// ---------------------------------------------------------------------------
+// BVH traversal, v4 (render_bvh4): v3 with the entry to visit next kept in a
+// register.  The reference pushes far then near and pops near at once; v4
+// continues with near in the register and pushes only far, popping when the
+// register is consumed — the same visiting order, one LDS store and load less
+// per interior visit, and at most depth - 1 stack entries (one pending far
+// child per level), so the LDS stack is `depth` slots instead of depth + 2:
+// config C's depth-32 tree fits 5 workgroups of 256 lanes per CU (5 waves per
+// SIMD, the register limit) instead of 4.
+// ---------------------------------------------------------------------------
+struct TravState4 {
+    int state;  // 1 traversing (cur valid), 0 idle, -1 finished (awaiting shade)
+    int cur;    // entry to visit next (record index >= 0, or ~leaf)
+    int sp;     // LDS stack entries
+    float best, bestK;
+    int bi;
+    bool fast;
+    SlabRay R;
+};
+
+__device__ __forceinline__ void begin_segment4(Lane& L, TravState4& T, int root) {
+    L.bounce += 1;
+    L.segs += 1;
+    T.best = 1e38f;
+    T.bestK = 1e38f * 1.0009765625f;
+    T.bi = -1;
+    T.R.o = L.o;
+    T.R.d = L.d;
+    T.R.sx = L.d.x < 1e-6f && L.d.x > -1e-6f;
+    T.R.sy = L.d.y < 1e-6f && L.d.y > -1e-6f;
+    T.R.sz = L.d.z < 1e-6f && L.d.z > -1e-6f;
+    T.R.y = mk(T.R.sx ? 0.0f : 1.0f / L.d.x, T.R.sy ? 0.0f : 1.0f / L.d.y, T.R.sz ? 0.0f : 1.0f / L.d.z);
+    T.fast = !(T.R.sx || T.R.sy || T.R.sz) && mk_coord_ok(L.o.x) && mk_coord_ok(L.o.y) && mk_coord_ok(L.o.z) &&
+             fabsf(L.d.x) <= 2.0f && fabsf(L.d.y) <= 2.0f && fabsf(L.d.z) <= 2.0f;
+    T.cur = root;
+    T.sp = 0;
+    T.state = 1;
+}
+
+// next entry: the top of the LDS stack, or the end of the traversal
+template <int BLOCK>
+__device__ __forceinline__ void bvh_pop4(TravState4& T, const int* st) {
+    if (T.sp > 0) {
+        T.sp -= 1;
+        T.cur = st[T.sp * BLOCK];
+    } else {
+        T.state = -1;
+    }
+}
+
+template <int BLOCK>
+__device__ __forceinline__ void bvh_interior4(TravState4& T, int* st, const float4* __restrict__ recs, bool fast,
+                                              int stack_slots, uint32_t& visits) {
+    visits++;
+    const float4* rp = recs + 4 * T.cur;
+    const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
+    const float4 r3 = rp[3];
+    float dA, dB;
+    if (fast) {
+        dA = slab_fast(T.R, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y);
+        dB = slab_fast(T.R, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w);
+    } else {
+        dA = slab<true>(T.R, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y);
+        dB = slab<true>(T.R, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w);
+    }
+    const int eA = __float_as_int(r3.x), eB = __float_as_int(r3.y);
+    const bool nearA = dA < dB;
+    const float dNear = nearA ? dA : dB;
+    const float dFar = nearA ? dB : dA;
+    const int iNear = nearA ? eA : eB;
+    const int iFar = nearA ? eB : eA;
+    // the reference's two pushes (far, then near) and the pop that follows
+    // (a valid tree never needs more than depth - 1 < stack_slots entries;
+    // the bound only keeps the store inside the lane's slots)
+    const bool pushFar = dFar < T.best;
+    const bool pushNear = dNear < T.best;
+    if (pushNear) {
+        if (pushFar && T.sp < stack_slots) st[(T.sp++) * BLOCK] = iFar;
+        T.cur = iNear;
+    } else if (pushFar) {
+        T.cur = iFar;
+    } else {
+        bvh_pop4<BLOCK>(T, st);
+    }
+}
+
+template <Bvh3Spec S>
+__global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves))) void render_bvh4(RenderParams p) {
+    constexpr int BLOCK = S.block, THRESH = S.thresh;
+    extern __shared__ int bvh_stack[];
+    int* st = bvh_stack + threadIdx.x;
+    const float4* __restrict__ recs = p.bvh_recs;
+    Lane L;
+    lane_init(L);
+    TravState4 T;
+    T.state = 0;
+    T.cur = 0;
+    T.sp = 0;
+    T.best = T.bestK = 1e38f;
+    T.bi = -1;
+    T.fast = true;
+    uint32_t tests = 0, visits = 0;
+    for (;;) {
+        if (T.state < 0) {
+            shade(L, p, T.best, T.bi);
+            T.state = 0;
+        }
+        advance(L, p);
+        if (L.st == ST_TRACE && T.state == 0) begin_segment4(L, T, p.bvh_root);
+        if (!__any(T.state > 0)) break;
+        const bool fast = p.recs_ok && __all(T.fast || T.state <= 0);
+        for (;;) {
+            // interior sub-step
+            if (T.state > 0 && T.cur >= 0) bvh_interior4<BLOCK>(T, st, recs, fast, p.stack_slots, visits);
+            // leaf sub-step (sees the near child just taken)
+            if (T.state > 0 && T.cur < 0) {
+                TravState3 t3;  // bvh_leaf3's view of the lane
+                t3.R = T.R;
+                t3.best = T.best;
+                t3.bestK = T.bestK;
+                t3.bi = T.bi;
+                bvh_leaf3(t3, T.cur, p.nodes, p.tri, tests);
+                T.best = t3.best;
+                T.bestK = t3.bestK;
+                T.bi = t3.bi;
+                bvh_pop4<BLOCK>(T, st);
+            }
+            const unsigned long long fin = __ballot(T.state < 0);
+            if (!__any(T.state > 0) || __popcll(fin) >= (unsigned)THRESH) break;
+        }
+    }
+    flush_counters(L, p);
+    unsigned long long t = tests, v = visits;
+    for (int off = 32; off > 0; off >>= 1) {
+        t += __shfl_xor(t, off);
+        v += __shfl_xor(v, off);
+    }
+    if (lane_id() == 0) {
+        atomicAdd(p.seg_counter + 1, t);  // leaf triangle tests
+        atomicAdd(p.seg_counter + 2, v);  // interior node visits (diagnostic)
+        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+        atomicMin(p.seg_counter + 5, t_end);
+        atomicMax(p.seg_counter + 6, t_end);
+    }
+}
+
 // Division check for div_mk (test hook): n, d drawn from the ranges above.
 __global__ void div_check_kernel(uint32_t seed, unsigned long long count, int mode, unsigned long long* bad,
                                  uint32_t* first) {

@@ -450,7 +450,7 @@ constexpr int kTileTris = 1024;  // 48 KiB of LDS per tile
 // product build carries the variants the launcher chooses automatically; the
 // A/B experiments measured in DESIGN.md ("Tried and measured") are compiled
 // only with -DRT2_EXPERIMENTS (make EXPERIMENTS=1).
-enum Kind : int { K_RESIDENT = 0, K_TILED = 1, K_SMEM = 2, K_SPLIT = 3, K_ASSIST = 4, K_BVH = 5, K_BVH2 = 6, K_BVH3 = 7 };
+enum Kind : int { K_RESIDENT = 0, K_TILED = 1, K_SMEM = 2, K_SPLIT = 3, K_ASSIST = 4, K_BVH = 5, K_BVH2 = 6, K_BVH3 = 7, K_BVH4 = 8 };
 struct Variant {
     int id;
     int kind;
@@ -504,7 +504,7 @@ constexpr Bvh3Spec bvh3_x(int t, Slab sl, int w, bool diag = false) {
 
 const Variant kVariants[] = {
     RT2_VARIANT(0, K_SMEM, render_smem<kSmemDefault>, 256, "smem/256/max3f8/coop32/w6/lockstep"),  // default (<= kSmemMaxTris)
-    RT2_VARIANT(53, K_BVH3, render_bvh3<kBvhDefault>, 256, "bvh3/256/t16/w5"),            // default (BVH traversal)
+    RT2_VARIANT(109, K_BVH4, render_bvh4<kBvhDefault>, 256, "bvh4/256/t16/w5"),           // default (BVH traversal)
     RT2_VARIANT(86, K_TILED, render_tiled<kTiledLarge>, 512, "tiled/512/max3f4"),          // > kSmemMaxTris
     RT2_VARIANT(92, K_ASSIST, render_assist<kAssist12>, 768, "assist12/max3f8/w6"),        // < 4 items per lane
 #ifdef RT2_EXPERIMENTS
@@ -512,6 +512,7 @@ const Variant kVariants[] = {
     RT2_VARIANT(85, K_SPLIT, render_split<kSplitSmall>, 256, "split4/max3f8/w6"),          // round-1 choice, < 1 item per lane
     RT2_VARIANT(90, K_ASSIST, render_assist<kAssist8>, 512, "assist8/max3f8/w6"),
     RT2_VARIANT(95, K_ASSIST, render_assist<assist12_x(48)>, 768, "assist12/max3f8/w6/coop48"),
+    RT2_VARIANT(53, K_BVH3, render_bvh3<kBvhDefault>, 256, "bvh3/256/t16/w5"),            // round-1/2 BVH default
     RT2_VARIANT(101, K_SMEM, render_smem<kSmemLock512>, 512, "smem/512/max3f8/coop32/w6/lockstep"),
     RT2_VARIANT(104, K_SMEM, render_smem<kSmemLock128>, 128, "smem/128/max3f8/coop32/w6/lockstep"),
     RT2_VARIANT(106, K_SMEM, render_smem<kSmemFree>, 256, "smem/256/max3f8/coop32/w6/free"),  // round-1 default
@@ -560,7 +561,7 @@ const Variant kVariants[] = {
 constexpr size_t kResidentMaxBytes = 112 * 1024;
 constexpr int kSmemMaxTris = 131072;  // scalar path up to 6.3 MB of records (config C: 781 vs 817 ms tiled; config E: tiled 1,704 vs 2,312 ms)
 constexpr int kDefaultBrute = 0;
-constexpr int kDefaultBvh = 53;
+constexpr int kDefaultBvh = 109;
 constexpr int kLargeScene = 86;  // tiled/512/max3f4: LDS tiles above kSmemMaxTris triangles
 constexpr int kSlab = 92;        // assist12/max3f8/w6: fewer than 4 items per lane (multi-GPU slabs)
 
@@ -807,8 +808,10 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
         lds = (size_t)3 * sizeof(float4) * kTileTris;
     else if (V.kind == K_RESIDENT)
         lds = resident_bytes;
-    else if (V.kind >= K_BVH)
+    else if (V.kind >= K_BVH) {
+        if (V.kind == K_BVH4) p.stack_slots = std::max(s->bvh_depth, 1);  // next entry in a register
         lds = (size_t)p.stack_slots * V.block * sizeof(int);
+    }
     p.bvh_recs = s->d_recs;
     p.bvh_root = s->bvh_root;
     p.recs_ok = s->recs_ok;

@@ -92,11 +92,12 @@ def test_bvh_requires_nodes_and_validates(rt2mod, torch_cuda):
         rt2mod.Scene(triangles=sd.triangles(), materials=sd.materials(), nodes=nodes)
 
 
-# render_bvh2 (child-pair records, Markstein slabs, while-while) and
-# render_bvh3 (+ wave-uniform fast slab path, fused interior/leaf sub-steps)
-# (53 = the product kernel; the others are experiment-build variants)
-BVH2_VARIANTS = [53] + ([40, 41, 43, 45, 46, 47, 48, 50, 54, 55] if EXPERIMENTS else [])
-BVH_SPOT = (53, 40, 46, 50, 55)
+# render_bvh2 (child-pair records, Markstein slabs, while-while),
+# render_bvh3 (+ wave-uniform fast slab path, fused interior/leaf sub-steps) and
+# render_bvh4 (+ the next entry in a register, depth-sized LDS stack)
+# (109 = the product kernel; the others are experiment-build variants)
+BVH2_VARIANTS = [109] + ([40, 41, 43, 45, 46, 47, 48, 50, 53, 54, 55] if EXPERIMENTS else [])
+BVH_SPOT = (109, 53, 40, 46, 50, 55)
 
 
 @pytest.mark.parametrize("mode", [0, 1])
