@@ -50,6 +50,9 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec
 FLOP_PER_TEST = 53
 FLOP_PER_VISIT = 24        # BVH interior node: 2 boxes x (6 sub + 6 div), compute.glsl:382-408
 BYTES_PER_TEST = 36        # a, b, c positions
+BVH_RECORD_BYTES = 64      # BVH: one child-pair record per interior visit (both boxes + entries)
+BVH_TRI_BYTES = 48         # BVH: one pre-transformed triangle record per leaf test
+L2_PEAK_GBS = 34500.0      # MI355X_MICROARCH.md §L2: ≈34.5 TB/s aggregate
 TARGET_RATIO = 10.0        # north star: >= 10x the CPU reference at config C on 1 GPU
 KERNEL_FILES = {"smem": "render_smem", "split": "render_split", "tiled": "render_tiled", "assist": "render_assist",
                 "resident": "render_resident", "bvh4": "render_bvh4", "bvh3": "render_bvh3", "bvh2": "render_bvh2",
@@ -124,13 +127,21 @@ def roofline(tests, visits, kern_ms):
     """FP32-VALU roofline of one launch: algorithmic FLOP / kernel time."""
     flops = (FLOP_PER_TEST * tests + FLOP_PER_VISIT * visits) / (kern_ms * 1e-3) / 1e12
     hbm = BYTES_PER_TEST * tests / (kern_ms * 1e-3) / 1e9
-    return {"bound": "valu", "achieved": round(flops, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(flops / VALU_PEAK_TFLOPS, 4), "traffic": None, "kernel_ms": round(kern_ms, 3),
-            "tests_per_launch": int(tests), "node_visits_per_launch": int(visits),
-            "flop_model": "53 x ray-triangle tests + 24 x BVH interior visits (2 slab boxes)",
-            "hbm_read_algorithmic": {"achieved": round(hbm, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                     "frac": round(hbm / HBM_PEAK_GBS, 3),
-                                     "note": "36 B x tests; >1 = on-chip reuse (effective bandwidth)"}}
+    rf = {"bound": "valu", "achieved": round(flops, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+          "frac": round(flops / VALU_PEAK_TFLOPS, 4), "traffic": None, "kernel_ms": round(kern_ms, 3),
+          "tests_per_launch": int(tests), "node_visits_per_launch": int(visits),
+          "flop_model": "53 x ray-triangle tests + 24 x BVH interior visits (2 slab boxes)",
+          "hbm_read_algorithmic": {"achieved": round(hbm, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                   "frac": round(hbm / HBM_PEAK_GBS, 3),
+                                   "note": "36 B x tests; >1 = on-chip reuse (effective bandwidth)"}}
+    if visits:
+        # the BVH walk is a chain of dependent per-lane gathers: its bound is
+        # the cache hierarchy, not the VALU (DESIGN.md §BVH traversal)
+        l2 = (BVH_RECORD_BYTES * visits + BVH_TRI_BYTES * tests) / (kern_ms * 1e-3) / 1e9
+        rf["l2_read_algorithmic"] = {"achieved": round(l2, 1), "peak": L2_PEAK_GBS, "unit": "GB/s",
+                                     "frac": round(l2 / L2_PEAK_GBS, 3),
+                                     "note": "64 B per interior visit + 48 B per leaf test, per-lane gathers"}
+    return rf
 
 
 def attach_traffic(rf, config, variant, kern_ms):
@@ -454,6 +465,8 @@ def main():
             "node_visits_per_segment": round(st2.node_visits / max(st2.segments, 1), 3),
             "valu_tflops": round((FLOP_PER_TEST * st2.tests + FLOP_PER_VISIT * st2.node_visits) / args.steps
                                  / (km2 * 1e-3) / 1e12, 3),
+            "l2_read_algorithmic_gbs": round((BVH_RECORD_BYTES * st2.node_visits + BVH_TRI_BYTES * st2.tests)
+                                             / args.steps / (km2 * 1e-3) / 1e9, 1) if st2.node_visits else None,
             "pixels_differing_from_main": ndiff,
             "rmse_vs_main": float(d2.pow(2).mean().sqrt()),
             "note": "brute force and the reference BVH traversal agree except on exact distance ties"}
