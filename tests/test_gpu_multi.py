@@ -144,3 +144,33 @@ def test_comm_gather_slabs_one_rank(rt2mod, config_scene, torch_cuda):
     comm.check()
     assert torch.equal(image, slab)
     comm.close()
+
+
+def test_torch_nccl_one_rank_gather(rt2mod, config_scene, torch_cuda):
+    """bench.py's multi-GPU gather (rt2/dist.py gather_image: dist.gather on the
+    nccl backend = RCCL) run for real on a one-rank process group: the gathered
+    and un-interleaved image equals the rank's own render bit for bit."""
+    import socket
+
+    import torch.distributed as dist
+    from rt2 import dist as rdist
+    torch = torch_cuda
+    sd, spec = config_scene("A")
+    W, H = 96, 40
+    u = rt2mod.offline_uniforms(W, H, 4, 2, sd.num_triangles)
+    scene = rt2mod.Scene(sd, 0)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        renderer = rdist.DeviceSlabRenderer(scene, u, 0, 2, 1, 0, 1)
+        slab = renderer().clone()
+        img = rdist.gather_image(renderer.image, H, W, 1, 0, 1)
+        torch.cuda.synchronize()
+        assert torch.equal(img, slab)
+        assert np.array_equal(img.cpu().numpy(), scene.render_host(u, 0, 2))
+    finally:
+        dist.destroy_process_group()
