@@ -38,21 +38,42 @@ template <int S = 1>
 __device__ __forceinline__ void advance(Lane& L, const RenderParams& p) {
     for (;;) {
         const bool need = L.st == ST_NEED_ITEM;
-        const unsigned long long m = __ballot(need);
+        unsigned long long m = __ballot(need);
         if (m) {
-            unsigned long long base = 0;
+            unsigned long long it = ~0ull;  // this lane's item (~0: none left)
             if constexpr (S == 1) {
-                if (lane_id() == 0) base = atomicAdd(p.item_counter, (unsigned long long)__popcll(m));
-                base = __shfl(base, 0);
+                if (p.region_ctr) {
+                    // 8 contiguous item regions, one per workgroup group b % 8
+                    // (the workgroups that share an XCD's L2): a group takes
+                    // items from its own region first, then from the others
+                    const uint32_t g0 = blockIdx.x & 7u;
+#pragma unroll 1
+                    for (uint32_t k = 0; k < 8u && m; k++) {
+                        const uint32_t r = (g0 + k) & 7u;
+                        const unsigned long long lo = p.n_items * r / 8u, hi = p.n_items * (r + 1u) / 8u;
+                        unsigned long long base = 0;
+                        if (lane_id() == 0) base = atomicAdd(p.region_ctr + 16u * r, (unsigned long long)__popcll(m));
+                        base = __shfl(base, 0);
+                        if ((m >> lane_id()) & 1ull) {
+                            const unsigned long long j = lo + base + lanes_below(m);
+                            if (j < hi) it = j;
+                        }
+                        m = __ballot(need && it == ~0ull);
+                    }
+                } else {
+                    unsigned long long base = 0;
+                    if (lane_id() == 0) base = atomicAdd(p.item_counter, (unsigned long long)__popcll(m));
+                    base = __shfl(base, 0);
+                    if (need) it = base + lanes_below(m);
+                }
             } else {
                 __shared__ unsigned long long split_base;
                 if (threadIdx.x == 0) split_base = atomicAdd(p.item_counter, (unsigned long long)__popcll(m));
                 __syncthreads();
-                base = split_base;
+                if (need) it = split_base + lanes_below(m);
                 __syncthreads();
             }
             if (need) {
-                unsigned long long it = base + lanes_below(m);
                 if (it < p.n_items) {
                     // frame_split: item = frame * n_pix + pixel (frame-major), so the
                     // last items of a launch are single pixel-frames

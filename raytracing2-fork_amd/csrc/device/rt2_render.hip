@@ -105,6 +105,7 @@ struct rt2_scene {
     uint4* d_host_acc8 = nullptr;   // 8-bit path sums
     uint8_t* d_host_rgb8 = nullptr; // 8-bit path result (3 B per pixel)
     size_t host_cap = 0;            // pixels the four buffers hold
+    unsigned long long* d_region_ctr = nullptr;  // 8 item-region counters, 128 B apart
     unsigned long long* wave_log = nullptr;  // diagnostic wave timeline (rt2_scene_set_wave_log)
     uint32_t wave_log_n = 0;
 };
@@ -425,6 +426,7 @@ extern "C" void rt2_scene_destroy(rt2_scene* s) {
     (void)hipFree(s->d_host_res);
     (void)hipFree(s->d_host_acc8);
     (void)hipFree(s->d_host_rgb8);
+    (void)hipFree(s->d_region_ctr);
     if (s->host_stream) (void)hipStreamDestroy(s->host_stream);
     delete s;
 }
@@ -700,6 +702,12 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     // stream that was issued on
     if (s->last_launch_valid) HIPCHECK(hipStreamWaitEvent(st, s->last_launch, 0));
     HIPCHECK(hipMemsetAsync(s->d_counters, 0, sizeof(unsigned long long), st));
+    // items in 8 contiguous regions, one per group of workgroups sharing an
+    // XCD's L2 (blockIdx % 8): neighbouring pixels' rays walk the same BVH
+    // lines in one L2 (config C BVH: 2,701 vs 2,783 ms; brute force ±0)
+    if (!s->d_region_ctr) HIPCHECK(hipMalloc(&s->d_region_ctr, 8 * 128));
+    HIPCHECK(hipMemsetAsync(s->d_region_ctr, 0, 8 * 128, st));
+    p.region_ctr = s->d_region_ctr;
     HIPCHECK(hipMemsetAsync(s->d_counters + 6, 0xff, sizeof(unsigned long long), st));  // diag: min wave end
     HIPCHECK(hipMemsetAsync(s->d_counters + 7, 0, sizeof(unsigned long long), st));     // diag: max wave end
     p.nodes = s->d_nodes;

@@ -43,6 +43,7 @@ struct RenderParams {
     float4* accum;
     uint4* accum8;
     unsigned long long* item_counter;
+    unsigned long long* region_ctr;  // nullable: 8 item-region counters, 128 B apart (XCD-group regions)
     unsigned long long* seg_counter;
     int tile_tris;  // TILED: triangles per LDS tile
     const rt2_node* nodes;  // BVH traversal

@@ -40,7 +40,9 @@ F = a.frames or spec.frames
 variants = [int(v) for v in a.variants.split(",")]
 times = {v: [] for v in variants}
 ref = None
+sha = {}  # image digest per variant (compare across runs, e.g. with different environments)
 import ctypes as C  # noqa: E402
+import hashlib  # noqa: E402
 diag = {}
 for rnd in range(a.rounds):
     for v in variants:
@@ -68,6 +70,7 @@ for rnd in range(a.rounds):
             if ref is None:
                 ref = img
             assert np.array_equal(img, ref), f"variant {v} differs"
+            sha[v] = hashlib.sha256(np.ascontiguousarray(img).tobytes()).hexdigest()[:16]
 st = scene.stats(reset=True)
 samples = W * H * R * F
 out = {}
@@ -77,4 +80,5 @@ for v in variants:
                                                         min_ms=round(min(times[v]) * 1e3, 2),
                                                         all_ms=[round(t * 1e3, 1) for t in times[v]],
                                                         msamples_s=round(samples / med / 1e6, 2))
-print(json.dumps({"config": a.config, "W": W, "H": H, "R": R, "variants": out, "diag": diag}, indent=1))
+print(json.dumps({"config": a.config, "W": W, "H": H, "R": R, "variants": out, "diag": diag, "image_sha256": sha},
+                 indent=1))
