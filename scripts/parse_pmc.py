@@ -46,8 +46,9 @@ def load(name):
 
 def main(config="B"):
     res = {}
-    for name in ("fetch", "write", "valu", "salu", "clock", "wait"):
-        res.update(load(name))
+    for name in ("fetch", "write", "valu", "salu", "clock", "wait", "l2"):
+        if os.path.isdir(os.path.join(OUT, f"pmc_{name}")):
+            res.update(load(name))
     out = {"config": config, "kernel_variant": bench_variant("fetch"),
            "kernel_source_sha256": kernel_source_digest("bvh" if config.endswith("_bvh") else "brute"), "counters_per_launch": res}
     if "FETCH_SIZE" in res and "WRITE_SIZE" in res:
@@ -63,6 +64,10 @@ def main(config="B"):
         out["kernel_ns_profiled"] = sum(durs) / len(durs)
         if "GRBM_GUI_ACTIVE" in res:
             out["effective_clock_ghz"] = res["GRBM_GUI_ACTIVE"] / 8 / out["kernel_ns_profiled"]
+    if "TCC_HIT_sum" in res and "TCC_MISS_sum" in res:
+        out["l2_hit_rate"] = res["TCC_HIT_sum"] / max(res["TCC_HIT_sum"] + res["TCC_MISS_sum"], 1.0)
+    if "SQ_THREAD_CYCLES_VALU" in res and "SQ_ACTIVE_INST_VALU" in res:
+        out["valu_lane_utilisation"] = res["SQ_THREAD_CYCLES_VALU"] / (64.0 * res["SQ_ACTIVE_INST_VALU"])
     if "SQ_ACTIVE_INST_VALU" in res and "SQ_WAVE_CYCLES" in res:
         out["valu_active_frac_of_wave_cycles"] = res["SQ_ACTIVE_INST_VALU"] / res["SQ_WAVE_CYCLES"]
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
