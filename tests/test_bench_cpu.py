@@ -1,0 +1,88 @@
+"""bench.py's measurement bookkeeping, on the CPU: the kernel-code digest that
+ties a PMC profile to the launched kernel, the traffic attachment rule
+(roofline.traffic only from a profile of the same variant and code), the
+roofline figures and the GPU/CPU summary."""
+import json
+import os
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def test_code_digest_ignores_comments_only():
+    src = "int a = 1; // one\n/* block\n comment */ float b = 2.0f;\n\n"
+    same = "int a = 1; // another note\n/* x */ float b = 2.0f;\n"
+    other = "int a = 2; // one\n/* block\n comment */ float b = 2.0f;\n"
+    assert bench._code_only(src) == bench._code_only(same)
+    assert bench._code_only(src) != bench._code_only(other)
+
+
+def test_digest_per_traversal():
+    b, v = bench.kernel_source_digest("brute"), bench.kernel_source_digest("bvh")
+    assert len(b) == 64 and len(v) == 64 and b != v
+    assert bench.kernel_source_digest("brute") == b  # deterministic
+
+
+@pytest.fixture
+def profile_dir(tmp_path, monkeypatch):
+    os.makedirs(tmp_path / "profiles")
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    monkeypatch.setattr(bench, "kernel_source_digest", lambda traversal="brute": f"digest-{traversal}")
+    return tmp_path / "profiles"
+
+
+def write_profile(d, config, variant, digest, hbm=1234560000):
+    with open(d / f"pmc_config{config}.json", "w") as f:
+        json.dump({"config": config, "kernel_variant": variant, "kernel_source_sha256": digest,
+                   "hbm_bytes_per_launch": hbm}, f)
+
+
+def test_traffic_attached_only_for_the_same_kernel(profile_dir):
+    rf = bench.roofline(1e9, 0, 100.0)
+    bench.attach_traffic(rf, "B", "smem/x", 100.0)
+    assert rf["traffic"] is None and "no PMC profile" in rf["traffic_note"]
+
+    write_profile(profile_dir, "B", "smem/x", "digest-brute")
+    rf = bench.roofline(1e9, 0, 100.0)
+    bench.attach_traffic(rf, "B", "smem/x", 100.0)
+    assert rf["traffic"] == 1234560000
+    assert rf["hbm_measured"]["achieved"] == pytest.approx(1234560000 / 0.1 / 1e9, rel=1e-3)
+
+    for variant, digest in (("smem/y", "digest-brute"), ("smem/x", "stale")):
+        write_profile(profile_dir, "B", variant, digest)
+        rf = bench.roofline(1e9, 0, 100.0)
+        bench.attach_traffic(rf, "B", "smem/x", 100.0)
+        assert rf["traffic"] is None and "not attached" in rf["traffic_note"]
+
+    # a BVH leg is matched against the BVH kernels' code digest
+    write_profile(profile_dir, "C_bvh", "bvh4/x", "digest-bvh", hbm=99)
+    rf = bench.roofline(1e6, 1e8, 50.0)
+    bench.attach_traffic(rf, "C_bvh", "bvh4/x", 50.0)
+    assert rf["traffic"] == 99
+
+
+def test_roofline_figures():
+    tests, kern_ms = 1.0214e12, 520.0
+    rf = bench.roofline(tests, 0, kern_ms)
+    flops = bench.FLOP_PER_TEST * tests / (kern_ms * 1e-3) / 1e12
+    assert rf["achieved"] == pytest.approx(flops, rel=1e-3)
+    assert rf["frac"] == pytest.approx(flops / bench.VALU_PEAK_TFLOPS, rel=1e-3)
+    assert rf["bound"] == "valu" and rf["unit"] == "TFLOP/s" and rf["traffic"] is None
+    assert "l2_read_algorithmic" not in rf  # brute force: no BVH gathers
+    rf = bench.roofline(9e9, 3.77e11, 2900.0)
+    l2 = (bench.BVH_RECORD_BYTES * 3.77e11 + bench.BVH_TRI_BYTES * 9e9) / 2.9 / 1e9
+    assert rf["l2_read_algorithmic"]["achieved"] == pytest.approx(l2, rel=1e-3)
+    assert rf["l2_read_algorithmic"]["peak"] == bench.L2_PEAK_GBS
+
+
+def test_kernel_labels():
+    assert bench.kernel_label("assist12/max3f8/w6").startswith("render_assist")
+    assert bench.kernel_label("bvh4/256/t16/w5").startswith("render_bvh4")
+    assert bench.kernel_label("bvh3/256/t16/w5").startswith("render_bvh3")
+    assert bench.kernel_label("smem/256/max3f8/coop32/w6/lockstep").startswith("render_smem")
+    assert bench.kernel_label(None) is None
