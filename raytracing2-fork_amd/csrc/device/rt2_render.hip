@@ -36,6 +36,7 @@ using namespace rt2d;
 #include "rt2_path.h"
 #include "rt2_brute.h"
 #include "rt2_assist.h"
+#include "rt2_mfma.h"
 #include "rt2_bvh.h"
 #include "rt2_misc_kernels.h"
 
@@ -69,6 +70,10 @@ struct rt2_scene {
     int plk_ok = 0;                             // sweep_plk usable: <= 1/64 of the triangles outside its range
     int plk_outside = 0;                        // triangles with an always-pass record
     float plk_A = 0.0f;                         // max |a_i| over the triangles
+    _Float16* d_mfma = nullptr;                 // render_mfma filter records (rt2_mfma.h)
+    float* d_mfma_tau = nullptr;                // per-triangle record scale
+    int mfma_ok = 0;                            // render_mfma usable (records built, scene in range)
+    float mfma_A = 0.0f;                        // max |a_i| over the in-range triangles
     float4* d_fb = nullptr;                     // frame_split scratch (per-frame colours)
     uchar4* d_texels = nullptr;                 // textures, RGBA8
     int4* d_tex_desc = nullptr;
@@ -399,6 +404,20 @@ static int scene_init(rt2_scene* s, const rt2_triangle* tris, int32_t n_tris, co
         s->plk_ok = (unsigned long long)flags[0] * 64 <= (unsigned long long)n_tris;  // <= 1/64 always-pass records
         std::memcpy(&s->plk_A, &flags[1], sizeof(float));
 #endif
+        // matrix-core filter records (render_mfma): 5 KiB per 16 triangles
+        const int n_pad = (n_tris + 15) / 16 * 16;
+        HIPCHECK(hipMalloc(&s->d_mfma, (size_t)n_pad * kMfmaQ * 32 * sizeof(_Float16)));
+        HIPCHECK(hipMalloc(&s->d_mfma_tau, (size_t)n_pad * sizeof(float)));
+        uint32_t* d_mflags = reinterpret_cast<uint32_t*>(s->d_counters + kCounters - 2);
+        HIPCHECK(hipMemset(d_mflags, 0, 2 * sizeof(uint32_t)));
+        hipLaunchKernelGGL(prep_mfma, dim3((n_pad + 255) / 256), dim3(256), 0, 0, s->d_tri, n_tris, n_pad, s->d_mfma,
+                           s->d_mfma_tau, d_mflags);
+        HIPCHECK(hipGetLastError());
+        uint32_t mflags[2];
+        HIPCHECK(hipMemcpy(mflags, d_mflags, sizeof(mflags), hipMemcpyDeviceToHost));
+        HIPCHECK(hipMemset(d_mflags, 0, 2 * sizeof(uint32_t)));
+        std::memcpy(&s->mfma_A, &mflags[1], sizeof(float));
+        s->mfma_ok = s->mfma_A <= 0x1p20f;
     }
     HIPCHECK(hipDeviceSynchronize());
     return 0;
@@ -414,6 +433,8 @@ extern "C" void rt2_scene_destroy(rt2_scene* s) {
     (void)hipFree(s->d_nodes);
     (void)hipFree(s->d_recs);
     (void)hipFree(s->d_plk);
+    (void)hipFree(s->d_mfma);
+    (void)hipFree(s->d_mfma_tau);
     (void)hipFree(s->d_fb);
     (void)hipFree(s->d_cost);
     (void)hipFree(s->d_order);
@@ -452,7 +473,10 @@ constexpr int kTileTris = 1024;  // 48 KiB of LDS per tile
 // product build carries the variants the launcher chooses automatically; the
 // A/B experiments measured in DESIGN.md ("Tried and measured") are compiled
 // only with -DRT2_EXPERIMENTS (make EXPERIMENTS=1).
-enum Kind : int { K_RESIDENT = 0, K_TILED = 1, K_SMEM = 2, K_SPLIT = 3, K_ASSIST = 4, K_BVH = 5, K_BVH2 = 6, K_BVH3 = 7, K_BVH4 = 8 };
+enum Kind : int {
+    K_RESIDENT = 0, K_TILED = 1, K_SMEM = 2, K_SPLIT = 3, K_ASSIST = 4, K_MFMA = 9,  // brute force
+    K_BVH = 5, K_BVH2 = 6, K_BVH3 = 7, K_BVH4 = 8                                     // BVH (kind >= K_BVH)
+};
 struct Variant {
     int id;
     int kind;
@@ -490,6 +514,7 @@ constexpr AssistSpec assist12_x(int coop) {
 #endif
 constexpr TiledSpec kTiledLarge{.block = 512, .group = 4, .filter = Filter::Max3};
 constexpr AssistSpec kAssist12{.waves_per_block = 12, .group = 8, .filter = Filter::Max3, .waves = 6, .coop_rays = 32};
+constexpr MfmaSpec kMfmaDefault{.block = 256, .waves = 2, .tail_lanes = 16};
 constexpr Bvh3Spec kBvhDefault{.block = 256, .thresh = 16, .slab = Slab::Markstein, .waves = 5, .diag = false};
 
 #ifdef RT2_EXPERIMENTS
@@ -509,6 +534,7 @@ const Variant kVariants[] = {
     RT2_VARIANT(109, K_BVH4, render_bvh4<kBvhDefault>, 256, "bvh4/256/t16/w5"),           // default (BVH traversal)
     RT2_VARIANT(86, K_TILED, render_tiled<kTiledLarge>, 512, "tiled/512/max3f4"),          // > kSmemMaxTris
     RT2_VARIANT(92, K_ASSIST, render_assist<kAssist12>, 768, "assist12/max3f8/w6"),        // < 4 items per lane
+    RT2_VARIANT(130, K_MFMA, render_mfma<kMfmaDefault>, 256, "mfma/256/f16x3/coop16/w2"),
 #ifdef RT2_EXPERIMENTS
     RT2_VARIANT(67, K_SMEM, render_smem<kSmemMid>, 256, "smem/256/max3f8/coop32"),         // round-1 choice, 1-4 items per lane
     RT2_VARIANT(85, K_SPLIT, render_split<kSplitSmall>, 256, "split4/max3f8/w6"),          // round-1 choice, < 1 item per lane
@@ -566,6 +592,8 @@ constexpr int kDefaultBrute = 0;
 constexpr int kDefaultBvh = 109;
 constexpr int kLargeScene = 86;  // tiled/512/max3f4: LDS tiles above kSmemMaxTris triangles
 constexpr int kSlab = 92;        // assist12/max3f8/w6: fewer than 4 items per lane (multi-GPU slabs)
+
+constexpr bool is_bvh(int kind) { return kind >= K_BVH && kind <= K_BVH4; }
 
 const Variant* find_variant(int id) {
     for (const Variant& v : kVariants)
@@ -651,6 +679,9 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     p.tri = s->d_tri;
     p.plk = s->plk_ok ? s->d_plk : nullptr;
     p.plk_A = s->plk_A;
+    p.mfma_frag = s->d_mfma;
+    p.mfma_tau = s->d_mfma_tau;
+    p.mfma_A = s->mfma_A;
     p.tri_mtl = s->d_mtl;
     p.raw = s->d_raw;
     p.texels = s->d_texels;
@@ -789,8 +820,9 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     // for small scenes (config B: 1,208 triangles), LDS-tiled sweep for large
     // ones (config E: 1M triangles)
     const Variant* VP = s->variant > 0 ? find_variant(s->variant) : nullptr;
-    if (VP && ((s->traversal == RT2_TRAVERSAL_BVH) != (VP->kind >= K_BVH))) VP = nullptr;
+    if (VP && ((s->traversal == RT2_TRAVERSAL_BVH) != is_bvh(VP->kind))) VP = nullptr;
     if (VP && VP->kind == K_RESIDENT && !fits) VP = nullptr;  // cannot hold this scene
+    if (VP && VP->kind == K_MFMA && !s->mfma_ok) VP = nullptr;  // scene outside the filter's range
     if (!VP && s->traversal == RT2_TRAVERSAL_BVH) VP = find_variant(kDefaultBvh);
     if (!VP) {
         int vi = s->n_tris <= kSmemMaxTris ? kDefaultBrute : kLargeScene;
@@ -816,14 +848,14 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
         lds = (size_t)3 * sizeof(float4) * kTileTris;
     else if (V.kind == K_RESIDENT)
         lds = resident_bytes;
-    else if (V.kind >= K_BVH) {
+    else if (is_bvh(V.kind)) {
         if (V.kind == K_BVH4) p.stack_slots = std::max(s->bvh_depth, 1);  // next entry in a register
         lds = (size_t)p.stack_slots * V.block * sizeof(int);
     }
     p.bvh_recs = s->d_recs;
     p.bvh_root = s->bvh_root;
     p.recs_ok = s->recs_ok;
-    s->last_kind = V.kind >= K_BVH ? K_BVH : V.kind;
+    s->last_kind = is_bvh(V.kind) ? K_BVH : V.kind;
     int occ = 0;
     HIPCHECK(variant_occupancy(V, &occ, lds));
     occ = std::max(occ, 1);

@@ -63,6 +63,9 @@ struct RenderParams {
     int assist_cap;              // ASSIST: waves per workgroup that take items (the others start as helpers)
     int assist_chunk;            // ASSIST: triangles per chunk of a posted sweep (a multiple of the group)
     int assist_nchunks;          // ASSIST: chunks per sweep (< 4096)
+    const void* mfma_frag;       // MFMA: f16 filter records [group][quantity][lane][8] (rt2_mfma.h)
+    const float* mfma_tau;       // MFMA: per-triangle record scale
+    float mfma_A;                // MFMA: max |a_i| over the in-range triangles
     unsigned long long* wave_log;  // nullable diagnostic: per wave {start, pool dry, end, segments} (ASSIST)
     uint32_t wave_log_n;           // waves the log holds
 };

@@ -295,7 +295,7 @@ def test_frame_split_identical(rt2mod, oraclemod, config_scene, torch_cuda, trav
 # the product variants (0, 86, 92) and, in an experiment build, the A/B
 # variants (masked/plk filters, resident LDS, cooperative and team tail modes,
 # split waves, the round-1 slab kernels, occupancy hints)
-BRUTE_VARIANTS = [0, 86, 92] + ([22, 24, 28, 52, 64, 65, 66, 67, 68, 70, 71, 72, 73, 74, 76, 79, 80, 84, 85, 87, 89, 95, 97, 101, 104, 106,
+BRUTE_VARIANTS = [0, 86, 92, 130] + ([22, 24, 28, 52, 64, 65, 66, 67, 68, 70, 71, 72, 73, 74, 76, 79, 80, 84, 85, 87, 89, 95, 97, 101, 104, 106,
                                  90] if EXPERIMENTS else [])
 
 
