@@ -135,10 +135,134 @@ static int pass_plk(f3 o, f3 d, const float* r, float A, float bestK) {
     return fmaxf(fmaxf(fmaxf(fmaxf(U, -V), X), -tn), Y) <= T;
 }
 
+/* ---- the matrix-core filter (rt2_mfma.h prep_mfma / sweep_mfma) ----------
+ * binary16 rounding (RNE, subnormals down to 2^-24, as the f32->f16 convert) */
+static double to_f16(double x) {
+    const double ax = fabs(x);
+    if (ax == 0.0 || isnan(x)) return x;
+    if (ax >= 65520.0) return x > 0 ? INFINITY : -INFINITY;
+    int e;
+    (void)frexp(ax, &e);                                  /* ax in [2^(e-1), 2^e) */
+    const double quantum = ax < 0x1p-14 ? 0x1p-24 : ldexp(1.0, e - 11);
+    return rint(x / quantum) * quantum;
+}
+enum { MQ = 5 };
+/* prep_mfma: one triangle's 5 x 32 f16 slots and its scale tau; 0 = out of range */
+static int mfma_record(f3 a, f3 e0, f3 e1, f3 n, double slot[MQ][32], double* tau_out, float* Aout) {
+    const float av[3] = {a.x, a.y, a.z}, e0v[3] = {e0.x, e0.y, e0.z}, e1v[3] = {e1.x, e1.y, e1.z},
+                nv[3] = {n.x, n.y, n.z};
+    double coef[MQ][10] = {{0}};
+    double tau = 1.0;
+    float A = 0.0f, M = 0.0f;
+    int ok = 1;
+    for (int k = 0; k < 3; k++) {
+        ok = ok && fabsf(av[k]) <= 0x1p20f;
+        A = fmaxf(A, fabsf(av[k]));
+        const float xs[3] = {e0v[k], e1v[k], nv[k]};
+        for (int j = 0; j < 3; j++) {
+            const float ax = fabsf(xs[j]);
+            ok = ok && (xs[j] == 0.0f || (ax >= 0x1p-100f && ax <= 0x1p20f));
+            M = fmaxf(M, ax);
+        }
+    }
+    ok = ok && M >= 0x1p-30f;
+    *Aout = A;
+    if (ok) {
+        int ex;
+        (void)frexpf(M, &ex);
+        const double s = ldexp(1.0, 1 - ex);
+        double E0[3], E1[3], N[3], P0[3], P1[3];
+        for (int k = 0; k < 3; k++) E0[k] = s * e0v[k], E1[k] = s * e1v[k], N[k] = s * nv[k];
+        P0[0] = (double)av[1] * E0[2] - (double)av[2] * E0[1];
+        P0[1] = (double)av[2] * E0[0] - (double)av[0] * E0[2];
+        P0[2] = (double)av[0] * E0[1] - (double)av[1] * E0[0];
+        P1[0] = (double)av[1] * E1[2] - (double)av[2] * E1[1];
+        P1[1] = (double)av[2] * E1[0] - (double)av[0] * E1[2];
+        P1[2] = (double)av[0] * E1[1] - (double)av[1] * E1[0];
+        const double AN = (double)av[0] * N[0] + (double)av[1] * N[1] + (double)av[2] * N[2];
+        for (int k = 0; k < 3; k++) {
+            coef[0][k] = -P1[k];
+            coef[0][3 + k] = E1[k];
+            coef[1][k] = P0[k];
+            coef[1][3 + k] = -E0[k];
+            coef[2][k] = P1[k] - P0[k] + 1.0009765625 * N[k];
+            coef[2][3 + k] = E0[k] - E1[k];
+            coef[3][6 + k] = -N[k];
+            coef[4][k] = N[k];
+        }
+        coef[3][9] = AN;
+        double mx = 0.0;
+        for (int q = 0; q < MQ; q++)
+            for (int c = 0; c < 10; c++) mx = fmax(mx, fabs(coef[q][c]));
+        int e2;
+        (void)frexp(mx, &e2);
+        tau = ldexp(1.0, 14 - e2);
+    }
+    for (int q = 0; q < MQ; q++) {
+        for (int k = 0; k < 32; k++) slot[q][k] = 0.0;
+        for (int c = 0; c < 10; c++) {
+            const double v = coef[q][c] * tau;
+            const double hi = to_f16((float)v);
+            const double lo = to_f16((float)(v - (double)(float)hi));
+            if (c < 9) slot[q][3 * c] = hi, slot[q][3 * c + 1] = hi, slot[q][3 * c + 2] = lo;
+            else slot[q][27] = hi, slot[q][28] = lo;
+        }
+    }
+    *tau_out = tau;
+    return ok;
+}
+/* sweep_mfma's decision for one (ray, triangle) pair in a wave whose other
+ * rays raise max|o| to Ow and max(|o|,|m|) to Mw, in a scene whose max |a| is
+ * As.  The accumulation of the 32 exact f16 products (+ C) in f32 is replaced
+ * by the exact sum moved by the worst-case f32 summation error (31 u Σ|p|)
+ * toward rejection: a pass here is a pass for any summation order. */
+static int pass_mfma(f3 o, f3 d, double slot[MQ][32], double tau, float As, float Ow, float Mw, float bestK) {
+    const f3 m = cross(d, o);
+    const float ao = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+    const float am = fmaxf(fmaxf(fabsf(m.x), fabsf(m.y)), fabsf(m.z));
+    const float Omax = fmaxf(ao, Ow);
+    const float mx = fmaxf(fmaxf(Omax, fmaxf(am, Mw)), 1.0f);
+    int ex;
+    (void)frexpf(mx, &ex);
+    const float sigma = ldexpf(1.0f, 14 - ex);
+    const float R0 = Omax + As + 1.0f;
+    const float Tw = sigma * (0x1p-10f * R0);
+    const float Cw = -0x1p-14f * sigma;
+    const float Bmax = 2.0f * R0;
+    const float comp[9] = {d.x, d.y, d.z, m.x, m.y, m.z, o.x, o.y, o.z};
+    double ray[32];
+    for (int c = 0; c < 9; c++) {
+        const float v = comp[c] * sigma;
+        const double hi = to_f16(v);
+        const double lo = to_f16(v - (float)hi);
+        ray[3 * c] = hi, ray[3 * c + 1] = lo, ray[3 * c + 2] = hi;
+    }
+    ray[27] = ray[28] = sigma;
+    ray[29] = ray[30] = ray[31] = 0.0;
+    const float Tl = (float)tau * Tw;
+    const float cd = (float)tau * Cw;
+    float qv[MQ], qe[MQ];
+    for (int q = 0; q < MQ; q++) {
+        double s = q == 4 ? cd : 0.0, sa = q == 4 ? fabs(cd) : 0.0;
+        for (int k = 0; k < 32; k++) {
+            const double p = ray[k] * slot[q][k];
+            s += p;
+            sa += fabs(p);
+        }
+        qv[q] = (float)s;
+        qe[q] = (float)(31.0 * 0x1p-24 * sa) + 0x1p-149f;
+    }
+    const float bk = bestK <= Bmax ? bestK : INFINITY;
+    const float Y = fmaf(bk, qv[4] + qe[4], -(qv[3] - qe[3]));
+    const float t = fmaxf(fmaxf(fmaxf(qv[0] + qe[0], qv[1] + qe[1]), fmaxf(qv[2] + qe[2], qv[3] + qe[3])), Y);
+    return t <= Tl;
+}
+
 int main(int argc, char** argv) {
     const long long n = argc > 1 ? atoll(argv[1]) : 1000000;
     s_rng = argc > 2 ? strtoull(argv[2], 0, 10) * 0x9E3779B97F4A7C15ull + 1 : 88172645463325252ull;
     long long accepts = 0, bad_old = 0, bad_new = 0, p_old = 0, p_new = 0, bad_plk = 0, p_plk = 0, p_plk_near = 0, p_old_near = 0;
+    long long bad_mfma = 0, p_mfma = 0, n_mfma = 0, p_mfma_near = 0, n_mfma_near = 0;
     for (long long it = 0; it < n; it++) {
         const int kind = (int)(next64() % 6);
         const int far = (next64() % 4) == 0;  /* small triangle far from the origin */
@@ -197,6 +321,23 @@ int main(int argc, char** argv) {
             if (ex && !fp) bad_plk++;
             if (!far) p_plk_near += fp, p_old_near += fo;
         }
+        /* matrix filter: rays in its range (|o| <= 2^20, |d| <= 1.0001); the
+         * wave's other rays and the scene's other triangles may be larger */
+        if (fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)) <= 0x1p20f &&
+            fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fabsf(d.z)) <= 1.0001f) {
+            double slot[MQ][32], tau;
+            float Am;
+            const int inr = mfma_record(a, e0, e1, nrm, slot, &tau, &Am);
+            const int wk = (int)(next64() % 4);
+            const float Ow = wk == 1 ? 0x1p20f * uni() : wk == 2 ? 2.0f * scale * uni() : 0.0f;
+            const float Mw = wk == 3 ? 0x1p20f * uni() : 0.0f;
+            const float As = inr ? fmaxf(Am, (next64() % 3) == 0 ? 0x1p20f * uni() : 0.0f) : 0x1p20f;
+            const int fm = pass_mfma(o, d, slot, tau, As, Ow, Mw, bestK);
+            n_mfma++;
+            p_mfma += fm;
+            if (!far && !wide && wk == 0 && inr) n_mfma_near++, p_mfma_near += fm;
+            if (ex && !fm) bad_mfma++;
+        }
         accepts += ex;
         if (!wide) {  /* pass counts (filter efficiency) at ordinary scales only */
             p_old += fo;
@@ -205,7 +346,8 @@ int main(int argc, char** argv) {
         if (ex && !fo) bad_old++;
         if (ex && !fn) bad_new++;
     }
-    printf("%lld %lld %lld %lld %lld %lld %lld %lld\n", n, accepts, bad_old, bad_new, p_old, p_new, bad_plk, p_plk);
+    printf("%lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld\n", n, accepts, bad_old, bad_new, p_old,
+           p_new, bad_plk, p_plk, bad_mfma, p_mfma, n_mfma, p_mfma_near, n_mfma_near);
     fprintf(stderr, "near-origin draws: pass_old %lld pass_plk %lld\n", p_old_near, p_plk_near);
     return 0;
 }

@@ -1,7 +1,10 @@
 """The brute-force kernel's division-free filters never reject a pair the
 reference's Möller–Trumbore test accepts (CPU restatement of rt2_sweep.h
-mt_pass / mt_pass3 and the per-ray precomputed plk_pass in binary32;
-proofs in DESIGN.md, "Exactness of the filter" and "The per-ray filter").  tests/filter_check/filter_check.c draws random and adversarial
+mt_pass / mt_pass3 and the per-ray precomputed plk_pass in binary32, and of
+the matrix-core filter of rt2_mfma.h: f16 hi/lo slots, exact products, the
+f32 accumulation moved by its worst-case error toward rejection; proofs in
+DESIGN.md, "Exactness of the filter", "The per-ray filter" and "The matrix
+filter").  tests/filter_check/filter_check.c draws random and adversarial
 rays (edges, vertices, grazing, best at the hit distance); a tightened
 filter mutant shows violations, so the harness is sensitive."""
 import os
@@ -22,8 +25,15 @@ def checker(tmp_path_factory):
 
 def _run(exe, n, seed):
     out = subprocess.run([exe, str(n), str(seed)], check=True, capture_output=True, text=True).stdout
-    pairs, accepts, bad_old, bad_new, p_old, p_new, bad_plk, p_plk = map(int, out.split())
-    return pairs, accepts, bad_old, bad_new, p_old, p_new, bad_plk, p_plk
+    v = list(map(int, out.split()))
+    return tuple(v[:8])
+
+
+def _run_mfma(exe, n, seed):
+    """(violations, passes, in-range draws, passes and draws at ordinary scales)
+    of the matrix-core filter (rt2_mfma.h)."""
+    out = subprocess.run([exe, str(n), str(seed)], check=True, capture_output=True, text=True).stdout
+    return tuple(map(int, out.split()))[8:]
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
@@ -63,3 +73,28 @@ def test_harness_detects_a_plk_threshold_without_margin(tmp_path):
     subprocess.run(["gcc", "-O2", "-std=c11", "-ffp-contract=off", "-o", exe, str(p), "-lm"], check=True)
     _, _, _, _, _, _, bad_plk, _ = _run(exe, 3_000_000, 1)
     assert bad_plk > 0
+
+
+@pytest.mark.parametrize("seed", [4, 5])
+def test_matrix_filter_conservative(checker, seed):
+    """sweep_mfma's skip decision, for rays inside its range in waves whose
+    other rays (and scenes whose other triangles) are up to 2^20 large."""
+    bad, passes, draws, p_near, n_near = _run_mfma(checker, 2_000_000, seed)
+    assert draws > 1_500_000 and n_near > 100_000
+    assert bad == 0
+    assert p_near < 0.8 * n_near  # it does reject on ordinary scales (adversarial draws aim at the triangles)
+
+
+@pytest.mark.parametrize("old,new", [
+    ("const float Tw = sigma * (0x1p-10f * R0);", "const float Tw = sigma * (0x1p-20f * R0);"),  # margin too thin
+    ("const float Cw = -0x1p-14f * sigma;", "const float Cw = 0x1p-14f * sigma;"),  # det bias the wrong way
+])
+def test_harness_detects_a_wrong_matrix_filter(tmp_path, old, new):
+    src = open(SRC).read()
+    assert old in src
+    p = tmp_path / "mut.c"
+    p.write_text(src.replace(old, new))
+    exe = str(tmp_path / "mut")
+    subprocess.run(["gcc", "-O2", "-std=c11", "-ffp-contract=off", "-o", exe, str(p), "-lm"], check=True)
+    bad, _, _, _, _ = _run_mfma(exe, 1_000_000, 1)
+    assert bad > 0
