@@ -53,8 +53,10 @@ BYTES_PER_TEST = 36        # a, b, c positions
 BVH_RECORD_BYTES = 64      # BVH: one child-pair record per interior visit (both boxes + entries)
 BVH_TRI_BYTES = 48         # BVH: one pre-transformed triangle record per leaf test
 L2_PEAK_GBS = 34500.0      # MI355X_MICROARCH.md §L2: ≈34.5 TB/s aggregate
+MFMA_F16_PEAK_TFLOPS = 2500.0  # MI355X dense F16/BF16 matrix peak (MI355X_MICROARCH.md; no sparsity)
+MFMA_FLOP_PER_PAIR = 320   # render_mfma: 5 quantities x 32 k-slots x 2 per (ray, triangle) pair (rt2_mfma.h)
 TARGET_RATIO = 10.0        # north star: >= 10x the CPU reference at config C on 1 GPU
-KERNEL_FILES = {"smem": "render_smem", "split": "render_split", "tiled": "render_tiled", "assist": "render_assist",
+KERNEL_FILES = {"mfma": "render_mfma", "smem": "render_smem", "split": "render_split", "tiled": "render_tiled", "assist": "render_assist",
                 "resident": "render_resident", "bvh4": "render_bvh4", "bvh3": "render_bvh3", "bvh2": "render_bvh2",
                 "bvh": "render_bvh"}
 
@@ -81,7 +83,8 @@ def parse():
 # code).  A PMC profile carries the digest of the sources it was measured on.
 KERNEL_SOURCES = ["raytracing2-fork_amd/csrc/device/rt2_math.h", "raytracing2-fork_amd/csrc/device/rt2_sweep.h",
                   "raytracing2-fork_amd/csrc/device/rt2_path.h", "include/rt2_pinned_math.h", "include/rt2.h"]
-KERNEL_SOURCES_BY_TRAVERSAL = {"brute": ["raytracing2-fork_amd/csrc/device/rt2_brute.h"],  # the 1-GPU kernels
+KERNEL_SOURCES_BY_TRAVERSAL = {"brute": ["raytracing2-fork_amd/csrc/device/rt2_brute.h",  # the 1-GPU kernels
+                                         "raytracing2-fork_amd/csrc/device/rt2_mfma.h"],
                                "bvh": ["raytracing2-fork_amd/csrc/device/rt2_bvh.h"]}
 
 
@@ -123,8 +126,12 @@ def kernel_label(variant):
     return variant
 
 
-def roofline(tests, visits, kern_ms):
-    """FP32-VALU roofline of one launch: algorithmic FLOP / kernel time."""
+def roofline(tests, visits, kern_ms, segments=0, n_tris=0, variant=None):
+    """Roofline of one launch.  Scalar-path / BVH kernels: FP32-VALU bound,
+    algorithmic FLOP / kernel time.  The matrix-core kernel (render_mfma): its
+    filter products on the MFMA pipe (320 FLOP per ray-triangle pair over the
+    16-padded triangle count) against the dense F16 peak, with the
+    reference-formulation VALU figure (53 FLOP per test) beside it."""
     flops = (FLOP_PER_TEST * tests + FLOP_PER_VISIT * visits) / (kern_ms * 1e-3) / 1e12
     hbm = BYTES_PER_TEST * tests / (kern_ms * 1e-3) / 1e9
     rf = {"bound": "valu", "achieved": round(flops, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -134,6 +141,18 @@ def roofline(tests, visits, kern_ms):
           "hbm_read_algorithmic": {"achieved": round(hbm, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                    "frac": round(hbm / HBM_PEAK_GBS, 3),
                                    "note": "36 B x tests; >1 = on-chip reuse (effective bandwidth)"}}
+    if variant and variant.startswith("mfma") and segments and n_tris:
+        pairs = segments * (-(-int(n_tris) // 16) * 16)
+        mf = MFMA_FLOP_PER_PAIR * pairs / (kern_ms * 1e-3) / 1e12
+        rf.update({"bound": "mfma", "achieved": round(mf, 3), "peak": MFMA_F16_PEAK_TFLOPS,
+                   "frac": round(mf / MFMA_F16_PEAK_TFLOPS, 4),
+                   "flop_model": "320 x (ray, triangle) pairs (5 f16x3 products of 32 k-slots per pair, triangles "
+                                 "padded to 16; rays = segments: the active lanes) on the matrix cores",
+                   "valu_algorithmic": {"achieved": round(flops, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                        "frac": round(flops / VALU_PEAK_TFLOPS, 4),
+                                        "note": "53 FLOP x tests (the reference formulation) / kernel time: the "
+                                                "rate the scalar-path kernels are measured in; the filter runs on "
+                                                "the matrix cores, so this is an effective figure"}})
     if visits:
         # the BVH walk is a chain of dependent per-lane gathers: its bound is
         # the cache hierarchy, not the VALU (DESIGN.md §BVH traversal)
@@ -291,7 +310,8 @@ def config_c_leg(torch, rt2, stream, threads, host, seconds, do_cpu):
             scene.render(u, 0, spec.frames, sh, accum.data_ptr(), 0, stream.cuda_stream)
         el, kern_ms, st = timed_renders(torch, rt2, scene, u, spec.frames, sh, accum, image, steps, stream)
         variant = launched_variant(rt2, scene)
-        rf = roofline(st.tests / steps, st.node_visits / steps, kern_ms)
+        rf = roofline(st.tests / steps, st.node_visits / steps, kern_ms, st.segments / steps, sd.num_triangles,
+                      variant)
         rf["kernel"] = kernel_label(variant)
         attach_traffic(rf, "C" if trav == "brute" else "C_bvh", variant, kern_ms)
         legs[trav] = {"value": round(samples * steps / el / 1e6, 4), "unit": "Msamples/s", "steps": steps,
@@ -411,7 +431,8 @@ def main():
             dist.destroy_process_group()
         return
 
-    rf = roofline(tests / args.steps / world, visits / args.steps / world, kern_ms)
+    rf = roofline(tests / args.steps / world, visits / args.steps / world, kern_ms, segs / args.steps / world,
+                  sd.num_triangles, variant)
     rf["kernel"] = kernel_label(variant)
     rf["segments_per_sample"] = round(segs / (samples_per_step * args.steps), 4)
     if world == 1:  # PMC traffic was measured for the 1-GPU launch

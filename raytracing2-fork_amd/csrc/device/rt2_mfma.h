@@ -41,6 +41,8 @@ struct MfmaSpec {
     int block;
     int waves;       // minimum waves per SIMD the register allocation must allow
     int tail_lanes;  // cooperative drain at <= this many live rays (pool dry)
+    bool imax = false;      // max of the five terms on their bit patterns (no NaN quieting; see sweep_mfma)
+    bool prefetch = false;  // the next group's records are requested before this group's products
 };
 
 // per wave: the ray fragments' staging rows (80-B stride: conflict-free
@@ -153,6 +155,7 @@ __device__ __forceinline__ float abs_max3(const f3& v) { return fmaxf(fmaxf(fabs
 // Closest hit of every lane's ray (o, d) over all triangles; the whole wave
 // calls it (lanes without a ray of their own carry a copy of a live one).
 // Returns false (nothing done) when a ray is outside the bound's range.
+template <MfmaSpec S>
 __device__ __forceinline__ bool sweep_mfma(const RenderParams& p, MfmaWaveLds& sh, const f3& o, const f3& d, float& best,
                                            int& bi, float& bestK) {
     const int lane = (int)lane_id();
@@ -200,27 +203,48 @@ __device__ __forceinline__ bool sweep_mfma(const RenderParams& p, MfmaWaveLds& s
 
     const h8* frag = reinterpret_cast<const h8*>(p.mfma_frag);
     const int ng = (p.n_tris + 15) >> 4;
-    for (int G = 0; G < ng; G++) {
+    h8 b0, b1, b2, b3, b4;
+    float tau;
+    auto fetch = [&](int G) {
         const h8* fg = frag + (size_t)G * (kMfmaQ * 64) + lane;
-        const h8 b0 = fg[0], b1 = fg[64], b2 = fg[128], b3 = fg[192], b4 = fg[256];
-        const float tau = p.mfma_tau[16 * G + (lane & 15)];
-        const float Tl = tau * Tw;
-        const float cd = tau * Cw;
+        b0 = fg[0], b1 = fg[64], b2 = fg[128], b3 = fg[192], b4 = fg[256];
+        tau = p.mfma_tau[16 * G + (lane & 15)];
+    };
+    if constexpr (S.prefetch) fetch(0);
+    for (int G = 0; G < ng; G++) {
+        if constexpr (!S.prefetch) fetch(G);
+        const h8 c0 = b0, c1 = b1, c2 = b2, c3 = b3, c4 = b4;
+        const float ct = tau;
+        if constexpr (S.prefetch) fetch(G + 1 < ng ? G + 1 : G);  // in flight during this group's products
+        const float Tl = ct * Tw;
+        const float cd = ct * Cw;
         const f4v zero = {0.0f, 0.0f, 0.0f, 0.0f};
         const f4v cdn = {cd, cd, cd, cd};
         unsigned long long M = 0;
 #pragma unroll
         for (int R = 0; R < 4; R++) {
-            const f4v qU = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[R], b0, zero, 0, 0, 0);
-            const f4v qV = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[R], b1, zero, 0, 0, 0);
-            const f4v qX = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[R], b2, zero, 0, 0, 0);
-            const f4v qT = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[R], b3, zero, 0, 0, 0);
-            const f4v qD = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[R], b4, cdn, 0, 0, 0);
+            const f4v qU = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[R], c0, zero, 0, 0, 0);
+            const f4v qV = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[R], c1, zero, 0, 0, 0);
+            const f4v qX = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[R], c2, zero, 0, 0, 0);
+            const f4v qT = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[R], c3, zero, 0, 0, 0);
+            const f4v qD = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[R], c4, cdn, 0, 0, 0);
 #pragma unroll
             for (int i = 0; i < 4; i++) {
                 const float Y = __builtin_fmaf(bk[R][i], qD[i], -qT[i]);
-                const float t = fmaxf(fmaxf(fmaxf(qU[i], qV[i]), fmaxf(qX[i], qT[i])), Y);
-                M |= __ballot(t <= Tl);
+                if constexpr (S.imax) {
+                    // t <= Tl (Tl > 0) on the bit patterns as signed integers:
+                    // negative floats are negative integers, positive floats
+                    // order like their patterns, so max_int(terms) <= int(Tl)
+                    // iff every term <= Tl.  A NaN term (Y = inf * 0 when
+                    // qD = 0, i.e. det < 0, which the reference rejects) may
+                    // pass or fail; no other term can be NaN (finite products).
+                    const int t3 = max(max(__float_as_int(qU[i]), __float_as_int(qV[i])), __float_as_int(qX[i]));
+                    const int t = max(max(t3, __float_as_int(qT[i])), __float_as_int(Y));  // two v_max3_i32
+                    M |= __ballot(t <= __float_as_int(Tl));
+                } else {
+                    const float t = fmaxf(fmaxf(fmaxf(qU[i], qV[i]), fmaxf(qX[i], qT[i])), Y);
+                    M |= __ballot(t <= Tl);
+                }
             }
         }
         if (M) {
@@ -295,7 +319,7 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
         const f3 ro = mine ? L.o : o, rd = mine ? L.d : dd;
         float best = 1e38f, bestK = 1e38f * 1.0009765625f;
         int bi = -1;
-        if (!sweep_mfma(p, sh, ro, rd, best, bi, bestK) && mine)
+        if (!sweep_mfma<S>(p, sh, ro, rd, best, bi, bestK) && mine)
             sweep_masked<8, true, Filter::Max3>(ro, rd, nullptr, (const float*)p.tri, p.n_tris, 0, best, bi, bestK);
         if (mine) {
             L.bounce += 1;

@@ -514,10 +514,15 @@ constexpr AssistSpec assist12_x(int coop) {
 #endif
 constexpr TiledSpec kTiledLarge{.block = 512, .group = 4, .filter = Filter::Max3};
 constexpr AssistSpec kAssist12{.waves_per_block = 12, .group = 8, .filter = Filter::Max3, .waves = 6, .coop_rays = 32};
-constexpr MfmaSpec kMfmaDefault{.block = 256, .waves = 2, .tail_lanes = 16};
+constexpr MfmaSpec kMfmaI{.block = 256, .waves = 2, .tail_lanes = 16, .imax = true};
 constexpr Bvh3Spec kBvhDefault{.block = 256, .thresh = 16, .slab = Slab::Markstein, .waves = 5, .diag = false};
 
 #ifdef RT2_EXPERIMENTS
+constexpr MfmaSpec kMfmaDefault{.block = 256, .waves = 2, .tail_lanes = 16};
+constexpr MfmaSpec kMfmaIP{.block = 256, .waves = 2, .tail_lanes = 16, .imax = true, .prefetch = true};
+constexpr MfmaSpec kMfmaP{.block = 256, .waves = 2, .tail_lanes = 16, .prefetch = true};
+constexpr MfmaSpec kMfmaI4{.block = 256, .waves = 4, .tail_lanes = 16, .imax = true};
+constexpr MfmaSpec kMfmaIP4{.block = 256, .waves = 4, .tail_lanes = 16, .imax = true, .prefetch = true};
 constexpr SmemSpec smem_x(int g, Filter f, Tail t, int lanes, int w, bool stats = false) {
     return SmemSpec{.block = 256, .group = g, .filter = f, .tail = t, .tail_lanes = lanes, .waves = w, .stats = stats};
 }
@@ -534,8 +539,14 @@ const Variant kVariants[] = {
     RT2_VARIANT(109, K_BVH4, render_bvh4<kBvhDefault>, 256, "bvh4/256/t16/w5"),           // default (BVH traversal)
     RT2_VARIANT(86, K_TILED, render_tiled<kTiledLarge>, 512, "tiled/512/max3f4"),          // > kSmemMaxTris
     RT2_VARIANT(92, K_ASSIST, render_assist<kAssist12>, 768, "assist12/max3f8/w6"),        // < 4 items per lane
-    RT2_VARIANT(130, K_MFMA, render_mfma<kMfmaDefault>, 256, "mfma/256/f16x3/coop16/w2"),
+    RT2_VARIANT(131, K_MFMA, render_mfma<kMfmaI>, 256, "mfma/256/f16x3/coop16/w2/imax"),  // default (<= kMfmaMaxTris)
+    RT2_VARIANT(136, K_SMEM, render_smem<kSmemDefault>, 256, "smem/256/max3f8/coop32/w6/lockstep"),  // variant 0 forced (id 0 = automatic)
 #ifdef RT2_EXPERIMENTS
+    RT2_VARIANT(130, K_MFMA, render_mfma<kMfmaDefault>, 256, "mfma/256/f16x3/coop16/w2"),      // f32 max (NaN quieting)
+    RT2_VARIANT(132, K_MFMA, render_mfma<kMfmaIP>, 256, "mfma/256/f16x3/coop16/w2/imax/pf"),
+    RT2_VARIANT(133, K_MFMA, render_mfma<kMfmaP>, 256, "mfma/256/f16x3/coop16/w2/pf"),
+    RT2_VARIANT(134, K_MFMA, render_mfma<kMfmaI4>, 256, "mfma/256/f16x3/coop16/w4/imax"),
+    RT2_VARIANT(135, K_MFMA, render_mfma<kMfmaIP4>, 256, "mfma/256/f16x3/coop16/w4/imax/pf"),
     RT2_VARIANT(67, K_SMEM, render_smem<kSmemMid>, 256, "smem/256/max3f8/coop32"),         // round-1 choice, 1-4 items per lane
     RT2_VARIANT(85, K_SPLIT, render_split<kSplitSmall>, 256, "split4/max3f8/w6"),          // round-1 choice, < 1 item per lane
     RT2_VARIANT(90, K_ASSIST, render_assist<kAssist8>, 512, "assist8/max3f8/w6"),
@@ -592,6 +603,8 @@ constexpr int kDefaultBrute = 0;
 constexpr int kDefaultBvh = 109;
 constexpr int kLargeScene = 86;  // tiled/512/max3f4: LDS tiles above kSmemMaxTris triangles
 constexpr int kSlab = 92;        // assist12/max3f8/w6: fewer than 4 items per lane (multi-GPU slabs)
+constexpr int kMfma = 131;       // mfma/256/f16x3/coop16/w2/imax: matrix-core filter (config B: 333 vs 530 ms)
+constexpr int kMfmaMaxTris = 16384;  // 5 MiB of f16 filter records: within reach of the L2s
 
 constexpr bool is_bvh(int kind) { return kind >= K_BVH && kind <= K_BVH4; }
 
@@ -816,9 +829,10 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     const size_t resident_bytes = (size_t)3 * sizeof(float4) * (size_t)std::max(s->n_tris, 1);
     const bool fits = resident_bytes <= kResidentMaxBytes;
     // explicit variant (rt2_scene_set_variant) when it exists in this build and
-    // matches the traversal; otherwise the automatic choice: scalar-path kernel
-    // for small scenes (config B: 1,208 triangles), LDS-tiled sweep for large
-    // ones (config E: 1M triangles)
+    // matches the traversal; otherwise the automatic choice: the matrix-core
+    // filter kernel for small scenes (config B: 1,208 triangles; the
+    // scalar-path kernel when the scene is outside its range), LDS-tiled sweep
+    // for large ones (config E: 1M triangles)
     const Variant* VP = s->variant > 0 ? find_variant(s->variant) : nullptr;
     if (VP && ((s->traversal == RT2_TRAVERSAL_BVH) != is_bvh(VP->kind))) VP = nullptr;
     if (VP && VP->kind == K_RESIDENT && !fits) VP = nullptr;  // cannot hold this scene
@@ -838,7 +852,10 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
             int occ0 = 0;
             HIPCHECK(variant_occupancy(*W, &occ0, 0));
             const unsigned long long lanes = (unsigned long long)s->num_cus * (unsigned long long)std::max(occ0, 1) * W->block;
-            if (p.n_items < 4 * lanes) vi = kSlab;
+            if (p.n_items < 4 * lanes)
+                vi = kSlab;
+            else if (s->mfma_ok && s->n_tris <= kMfmaMaxTris && find_variant(kMfma))
+                vi = kMfma;  // the filter on the matrix cores (rt2_mfma.h; DESIGN.md "The matrix filter")
         }
         VP = find_variant(vi);
     }

@@ -10,7 +10,7 @@ timeout -k 10 360 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; exit 1; }
 timeout -k 10 420 python bench.py ${BENCH_ARGS} > gpurun_out/bench.log 2>&1 || { echo "bench failed"; exit 1; }
 if [ -n "${SHARD_PROBE}" ]; then
-  timeout -k 10 120 python scripts/shard_probe.py --variants 0 > gpurun_out/shard.log 2>&1 || { echo "shard probe failed"; exit 1; }
+  timeout -k 10 120 python scripts/shard_probe.py --variants ${SHARD_VARIANTS:-0} > gpurun_out/shard.log 2>&1 || { echo "shard probe failed"; exit 1; }
 fi
 if [ -n "${REHEARSE_D}" ]; then
   RT2_BENCH_BACKEND=gloo timeout -k 10 180 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \

@@ -80,6 +80,22 @@ def test_roofline_figures():
     assert rf["l2_read_algorithmic"]["peak"] == bench.L2_PEAK_GBS
 
 
+def test_roofline_matrix_kernel():
+    """render_mfma: matrix FLOP over the 16-padded triangle count of each
+    segment against the dense F16 peak; the VALU-equivalent figure beside."""
+    segs, n, kern_ms = 8.45e8, 1208, 417.0
+    rf = bench.roofline(segs * n, 0, kern_ms, segs, n, "mfma/256/f16x3/coop16/w2")
+    mf = bench.MFMA_FLOP_PER_PAIR * segs * 1216 / (kern_ms * 1e-3) / 1e12
+    assert rf["bound"] == "mfma" and rf["peak"] == bench.MFMA_F16_PEAK_TFLOPS
+    assert rf["achieved"] == pytest.approx(mf, rel=1e-3)
+    assert rf["frac"] == pytest.approx(mf / bench.MFMA_F16_PEAK_TFLOPS, rel=1e-3)
+    v = bench.FLOP_PER_TEST * segs * n / (kern_ms * 1e-3) / 1e12
+    assert rf["valu_algorithmic"]["achieved"] == pytest.approx(v, rel=1e-3)
+    # other kernels keep the VALU roofline even when given segments
+    assert bench.roofline(segs * n, 0, kern_ms, segs, n, "smem/x")["bound"] == "valu"
+    assert bench.kernel_label("mfma/256/f16x3/coop16/w2/imax").startswith("render_mfma")
+
+
 def test_kernel_labels():
     assert bench.kernel_label("assist12/max3f8/w6").startswith("render_assist")
     assert bench.kernel_label("bvh4/256/t16/w5").startswith("render_bvh4")

@@ -6,13 +6,21 @@ not a multiple of the 16-triangle group and on the cooperative drain."""
 import numpy as np
 import pytest
 
-from conftest import require_variant
+from conftest import EXPERIMENTS, require_variant
 
 from test_gpu_parity import assert_exact, oracle_mean
 
 pytestmark = pytest.mark.gpu
 
-MFMA = 130
+MFMA = 131
+# product kernel (integer max of the terms); experiment build: f32 max, record
+# prefetch, 4 waves per SIMD
+VARIANTS = [131] + ([130, 132, 133, 134, 135] if EXPERIMENTS else [])
+
+
+@pytest.fixture(params=VARIANTS, ids=lambda v: f"v{v}")
+def mfma_variant(request):
+    return request.param
 
 
 @pytest.fixture(scope="module")
@@ -23,17 +31,17 @@ def torch_cuda():
     return torch
 
 
-def mfma_scene(rt2mod, sd=None, **kw):
+def mfma_scene(rt2mod, sd=None, variant=MFMA, **kw):
+    require_variant(rt2mod, variant)
     scene = rt2mod.Scene(sd, 0) if sd is not None else rt2mod.Scene(**kw)
-    scene.set_variant(MFMA)
+    scene.set_variant(variant)
     return scene
 
 
-def test_config_A_full_frame(rt2mod, oraclemod, config_scene, torch_cuda):
-    require_variant(rt2mod, MFMA)
+def test_config_A_full_frame(rt2mod, oraclemod, config_scene, torch_cuda, mfma_variant):
     sd, spec = config_scene("A")
     u = rt2mod.offline_uniforms(spec.width, spec.height, spec.bounces, spec.rays, sd.num_triangles)
-    scene = mfma_scene(rt2mod, sd)
+    scene = mfma_scene(rt2mod, sd, mfma_variant)
     img = scene.render_host(u, 0, spec.frames)
     st = scene.stats(reset=True)
     ref, _, segs = oracle_mean(oraclemod, sd, u, np.arange(spec.height), 0, spec.frames)
@@ -41,29 +49,26 @@ def test_config_A_full_frame(rt2mod, oraclemod, config_scene, torch_cuda):
     assert st.segments == segs
 
 
-def test_config_B_full_size_rows(rt2mod, oraclemod, config_scene, torch_cuda):
-    require_variant(rt2mod, MFMA)
+def test_config_B_full_size_rows(rt2mod, oraclemod, config_scene, torch_cuda, mfma_variant):
     sd, spec = config_scene("B")
     u = rt2mod.offline_uniforms(spec.width, spec.height, spec.bounces, spec.rays, sd.num_triangles)
-    scene = mfma_scene(rt2mod, sd)
+    scene = mfma_scene(rt2mod, sd, mfma_variant)
     img = scene.render_host(u, 0, spec.frames)
     rows = np.arange(2, 1080, 67, dtype=np.int32)
     ref, _, _ = oracle_mean(oraclemod, sd, u, rows, 0, spec.frames)
     assert_exact(img[rows], ref, "mfma config B rows")
 
 
-def test_config_C_small_image(rt2mod, oraclemod, config_scene, torch_cuda):
-    require_variant(rt2mod, MFMA)
+def test_config_C_small_image(rt2mod, oraclemod, config_scene, torch_cuda, mfma_variant):
     sd, spec = config_scene("C")
     u = rt2mod.offline_uniforms(48, 27, spec.bounces, 2, sd.num_triangles)
-    scene = mfma_scene(rt2mod, sd)
+    scene = mfma_scene(rt2mod, sd, mfma_variant)
     img = scene.render_host(u, 0, 1)
     ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(27), 0, 1)
     assert_exact(img, ref, "mfma config C")
 
 
-def test_diverse_materials(rt2mod, oraclemod, torch_cuda):
-    require_variant(rt2mod, MFMA)
+def test_diverse_materials(rt2mod, oraclemod, torch_cuda, mfma_variant):
     M = rt2mod.Material
     sd = rt2mod.SceneData()
     ids = [sd.add_material(m) for m in (M.diffuse((1, 0, 0)), M.diffuse((0, 1, 0)), M.diffuse((1, 1, 1)),
@@ -72,18 +77,17 @@ def test_diverse_materials(rt2mod, oraclemod, torch_cuda):
                                         M.specular((0.8, 0.6, 0.3), (1, 1, 1), 0.7, 0.4))]
     sd.create_diverse_cornell_box(10.0, *ids)
     u = rt2mod.offline_uniforms(80, 60, 12, 3, sd.num_triangles)
-    img = mfma_scene(rt2mod, sd).render_host(u, 0, 2)
+    img = mfma_scene(rt2mod, sd, mfma_variant).render_host(u, 0, 2)
     ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(60), 0, 2)
     assert_exact(img, ref, "mfma diverse")
 
 
 @pytest.mark.parametrize("case", ["ragged", "tiny_and_huge", "far_camera", "one"])
-def test_range_edges(rt2mod, oraclemod, torch_cuda, case):
+def test_range_edges(rt2mod, oraclemod, torch_cuda, case, mfma_variant):
     """Random triangle soups around a light: 1, 37 and 300 triangles (ragged
     last group); triangles with 1e-30 / 3e6 coordinates (out of the validated
     range: always-pass records); a camera 2^21 away (rays out of range: the
     scalar-path fallback)."""
-    require_variant(rt2mod, MFMA)
     M = rt2mod.Material
     rng = np.random.default_rng({"ragged": 1, "tiny_and_huge": 2, "far_camera": 3, "one": 4}[case])
     n = {"ragged": 37, "tiny_and_huge": 300, "far_camera": 300, "one": 1}[case]
@@ -102,7 +106,7 @@ def test_range_edges(rt2mod, oraclemod, torch_cuda, case):
     u = rt2mod.offline_uniforms(40, 30, 6, 3, n)
     if case == "far_camera":
         u.cameraPos.z = float(2 ** 21)
-    scene = mfma_scene(rt2mod, triangles=sd.triangles(), materials=sd.materials())
+    scene = mfma_scene(rt2mod, variant=mfma_variant, triangles=sd.triangles(), materials=sd.materials())
     img = scene.render_host(u, 0, 1)
     ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(30), 0, 1)
     assert_exact(img, ref, f"mfma {case}")
