@@ -46,7 +46,7 @@ def load(name):
 
 def main(config="B"):
     res = {}
-    for name in ("fetch", "write", "valu", "salu", "clock", "wait", "l2"):
+    for name in ("fetch", "write", "valu", "salu", "clock", "wait", "l2", "mfma"):
         if os.path.isdir(os.path.join(OUT, f"pmc_{name}")):
             res.update(load(name))
     out = {"config": config, "kernel_variant": bench_variant("fetch"),
@@ -70,6 +70,9 @@ def main(config="B"):
         out["valu_lane_utilisation"] = res["SQ_THREAD_CYCLES_VALU"] / (64.0 * res["SQ_ACTIVE_INST_VALU"])
     if "SQ_ACTIVE_INST_VALU" in res and "SQ_WAVE_CYCLES" in res:
         out["valu_active_frac_of_wave_cycles"] = res["SQ_ACTIVE_INST_VALU"] / res["SQ_WAVE_CYCLES"]
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in res and "GRBM_GUI_ACTIVE" in res:
+        # busy cycles summed over the SIMDs (1,024) vs the kernel's GPU cycles (GRBM_GUI_ACTIVE is per XCD x 8)
+        out["mfma_busy_frac"] = res["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * res["GRBM_GUI_ACTIVE"] / 8)
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     path = os.path.join(ROOT, "profiles", f"pmc_config{config}.json")
     with open(path, "w") as f:

@@ -16,5 +16,6 @@ run valu SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES && \
 run salu SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVES && \
 run clock GRBM_GUI_ACTIVE GRBM_COUNT && \
 run wait SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY && \
+{ [ -z "${EXTRA_MFMA}" ] || run mfma SQ_VALU_MFMA_BUSY_CYCLES SQ_VALU_MFMA_COEXEC_CYCLES SQ_INSTS_VALU SQ_WAVE_CYCLES; } && \
 { [ -z "${EXTRA_L2}" ] || run l2 TCC_HIT_sum TCC_MISS_sum SQ_THREAD_CYCLES_VALU SQ_INSTS_VMEM_RD; } && \
 echo "pmc ok"
