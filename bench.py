@@ -56,7 +56,7 @@ L2_PEAK_GBS = 34500.0      # MI355X_MICROARCH.md §L2: ≈34.5 TB/s aggregate
 MFMA_F16_PEAK_TFLOPS = 2500.0  # MI355X dense F16/BF16 matrix peak (MI355X_MICROARCH.md; no sparsity)
 MFMA_FLOP_PER_PAIR = 320   # render_mfma: 5 quantities x 32 k-slots x 2 per (ray, triangle) pair (rt2_mfma.h)
 TARGET_RATIO = 10.0        # north star: >= 10x the CPU reference at config C on 1 GPU
-KERNEL_FILES = {"mfma": "render_mfma", "smem": "render_smem", "split": "render_split", "tiled": "render_tiled", "assist": "render_assist",
+KERNEL_FILES = {"mfma": "render_mfma", "massist": "render_assist", "smem": "render_smem", "split": "render_split", "tiled": "render_tiled", "assist": "render_assist",
                 "resident": "render_resident", "bvh4": "render_bvh4", "bvh3": "render_bvh3", "bvh2": "render_bvh2",
                 "bvh": "render_bvh"}
 
@@ -83,8 +83,9 @@ def parse():
 # code).  A PMC profile carries the digest of the sources it was measured on.
 KERNEL_SOURCES = ["raytracing2-fork_amd/csrc/device/rt2_math.h", "raytracing2-fork_amd/csrc/device/rt2_sweep.h",
                   "raytracing2-fork_amd/csrc/device/rt2_path.h", "include/rt2_pinned_math.h", "include/rt2.h"]
-KERNEL_SOURCES_BY_TRAVERSAL = {"brute": ["raytracing2-fork_amd/csrc/device/rt2_brute.h",  # the 1-GPU kernels
-                                         "raytracing2-fork_amd/csrc/device/rt2_mfma.h"],
+KERNEL_SOURCES_BY_TRAVERSAL = {"brute": ["raytracing2-fork_amd/csrc/device/rt2_brute.h",  # the brute-force kernels
+                                         "raytracing2-fork_amd/csrc/device/rt2_mfma.h",
+                                         "raytracing2-fork_amd/csrc/device/rt2_assist.h"],
                                "bvh": ["raytracing2-fork_amd/csrc/device/rt2_bvh.h"]}
 
 
@@ -141,7 +142,7 @@ def roofline(tests, visits, kern_ms, segments=0, n_tris=0, variant=None):
           "hbm_read_algorithmic": {"achieved": round(hbm, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                    "frac": round(hbm / HBM_PEAK_GBS, 3),
                                    "note": "36 B x tests; >1 = on-chip reuse (effective bandwidth)"}}
-    if variant and variant.startswith("mfma") and segments and n_tris:
+    if variant and variant.startswith(("mfma", "massist")) and segments and n_tris:
         pairs = segments * (-(-int(n_tris) // 16) * 16)
         mf = MFMA_FLOP_PER_PAIR * pairs / (kern_ms * 1e-3) / 1e12
         rf.update({"bound": "mfma", "achieved": round(mf, 3), "peak": MFMA_F16_PEAK_TFLOPS,

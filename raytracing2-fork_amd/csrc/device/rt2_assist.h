@@ -36,9 +36,17 @@ struct AssistSpec {
     Filter filter;
     int waves;       // minimum waves per SIMD the register allocation must allow
     int coop_rays;   // with helpers: ray jobs for at most this many live rays (chunk jobs above)
+    bool mfma = false;    // sweeps and chunk units through the matrix filter (rt2_mfma.h sweep_mfma)
+    bool minred = false;  // its one-compare-per-group form
 };
 
-template <int NW>
+template <AssistSpec S>
+constexpr MfmaSpec assist_mfma_spec() {
+    return MfmaSpec{.block = 64 * S.waves_per_block, .waves = S.waves, .tail_lanes = 16, .imax = true,
+                    .minred = S.minred};
+}
+
+template <int NW, bool M = false>
 struct AssistLds {
     float ray[NW][6][64];            // posted rays, [wave][o.xyz d.xyz][lane]
     unsigned long long res[NW][64];  // per-lane closest-hit key of the job
@@ -47,6 +55,7 @@ struct AssistLds {
     uint32_t done[NW];               // units finished
     int busy;                        // waves that may still post jobs
     int helpers;                     // waves in the helper loop
+    MfmaWaveLds mw[M ? NW : 0];      // matrix filter: each wave's ray-fragment staging
 };
 
 __device__ __forceinline__ unsigned long long hit_key(float best, int bi) {
@@ -76,7 +85,7 @@ __device__ __forceinline__ uint32_t assist_claim(uint32_t* ticket) {
 
 // Runs one claimed unit (ticket value t) of job `s`.
 template <AssistSpec S, int NW>
-__device__ __forceinline__ void assist_unit(const RenderParams& p, AssistLds<NW>& sh, int s, uint32_t t) {
+__device__ __forceinline__ void assist_unit(const RenderParams& p, AssistLds<NW, S.mfma>& sh, int w, int s, uint32_t t) {
     const int lane = (int)lane_id();
     const int u = (int)(t & 0xfffu);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -93,8 +102,13 @@ __device__ __forceinline__ void assist_unit(const RenderParams& p, AssistLds<NW>
         const int lo = u * p.assist_chunk, hi = min(lo + p.assist_chunk, p.n_tris);
         float best = 1e38f, bestK = 1e38f * 1.0009765625f;
         int bi = -1;
-        sweep_masked<S.group, true, S.filter>(mk(r[0], r[64], r[128]), mk(r[192], r[256], r[320]), nullptr,
-                                              (const float*)p.tri + 12 * (size_t)lo, hi - lo, lo, best, bi, bestK);
+        const f3 ro = mk(r[0], r[64], r[128]), rd = mk(r[192], r[256], r[320]);
+        bool done = false;
+        if constexpr (S.mfma)  // chunks are whole 16-triangle groups; posted idle lanes carry a live ray
+            done = sweep_mfma<assist_mfma_spec<S>()>(p, sh.mw[w], ro, rd, best, bi, bestK, lo >> 4, (hi + 15) >> 4);
+        if (!done)
+            sweep_masked<S.group, true, S.filter>(ro, rd, nullptr, (const float*)p.tri + 12 * (size_t)lo, hi - lo, lo,
+                                                  best, bi, bestK);
         if (bi >= 0) atomicMin(&sh.res[s][lane], hit_key(best, bi));
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -104,7 +118,8 @@ __device__ __forceinline__ void assist_unit(const RenderParams& p, AssistLds<NW>
 // Serves units of this workgroup's jobs (own job first).  own >= 0: until
 // job `own` (of `units` units) is complete; own < 0: until no wave is busy.
 template <AssistSpec S, int NW>
-__device__ __forceinline__ void assist_work(const RenderParams& p, AssistLds<NW>& sh, int w, int own, uint32_t units) {
+__device__ __forceinline__ void assist_work(const RenderParams& p, AssistLds<NW, S.mfma>& sh, int w, int own,
+                                            uint32_t units) {
     constexpr int WG = __HIP_MEMORY_SCOPE_WORKGROUP;
     for (;;) {
         bool any = false;
@@ -113,7 +128,7 @@ __device__ __forceinline__ void assist_work(const RenderParams& p, AssistLds<NW>
             const int s = (w + k) % NW;
             const uint32_t t = assist_claim(&sh.ticket[s]);
             if (t != 0xffffffffu) {
-                assist_unit<S, NW>(p, sh, s, t);
+                assist_unit<S, NW>(p, sh, w, s, t);
                 any = true;
             }
         }
@@ -134,7 +149,7 @@ __global__ __launch_bounds__(64 * S.waves_per_block) __attribute__((amdgpu_waves
     RenderParams p) {
     constexpr int NW = S.waves_per_block;
     constexpr int WG = __HIP_MEMORY_SCOPE_WORKGROUP;
-    __shared__ AssistLds<NW> sh;
+    __shared__ AssistLds<NW, S.mfma> sh;
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = (int)(threadIdx.x & 63);
     const int cap = min(max(p.assist_cap, 1), NW);
@@ -165,14 +180,28 @@ __global__ __launch_bounds__(64 * S.waves_per_block) __attribute__((amdgpu_waves
             const bool chunk_job = !ray_job && helped && p.assist_nchunks > 1;
             float best = 1e38f, bestK = 1e38f * 1.0009765625f;
             int bi = -1;
+            // matrix filter: lanes without a ray carry the first live lane's
+            // (in range, so the wave keeps the matrix filter; their passes add
+            // no triangle and their results are not read)
+            f3 po = L.o, pd = L.d;
+            if constexpr (S.mfma) {
+                const int j0 = __builtin_ctzll(act);
+                if (L.st != ST_TRACE) {
+                    po = mk(__shfl(L.o.x, j0), __shfl(L.o.y, j0), __shfl(L.o.z, j0));
+                    pd = mk(__shfl(L.d.x, j0), __shfl(L.d.y, j0), __shfl(L.d.z, j0));
+                } else {
+                    (void)__shfl(L.o.x, j0), (void)__shfl(L.o.y, j0), (void)__shfl(L.o.z, j0);
+                    (void)__shfl(L.d.x, j0), (void)__shfl(L.d.y, j0), (void)__shfl(L.d.z, j0);
+                }
+            }
             if (ray_job || chunk_job) {
                 float* r = &sh.ray[w][0][lane];
-                r[0] = L.o.x;
-                r[64] = L.o.y;
-                r[128] = L.o.z;
-                r[192] = L.d.x;
-                r[256] = L.d.y;
-                r[320] = L.d.z;
+                r[0] = po.x;
+                r[64] = po.y;
+                r[128] = po.z;
+                r[192] = pd.x;
+                r[256] = pd.y;
+                r[320] = pd.z;
                 sh.res[w][lane] = ~0ull;
                 if (L.st == ST_TRACE) sh.list[w][lanes_below(act)] = (uint8_t)lane;
                 const uint32_t units = ray_job ? live : (uint32_t)p.assist_nchunks;
@@ -188,6 +217,10 @@ __global__ __launch_bounds__(64 * S.waves_per_block) __attribute__((amdgpu_waves
                     best = __uint_as_float((uint32_t)(key >> 32));
                     bi = (int)(uint32_t)key;
                 }
+            } else if constexpr (S.mfma) {
+                if (!sweep_mfma<assist_mfma_spec<S>()>(p, sh.mw[w], po, pd, best, bi, bestK) && L.st == ST_TRACE)
+                    sweep_masked<S.group, true, S.filter>(L.o, L.d, nullptr, (const float*)p.tri, p.n_tris, 0, best,
+                                                          bi, bestK);
             } else if (L.st == ST_TRACE) {
                 sweep_masked<S.group, true, S.filter>(L.o, L.d, nullptr, (const float*)p.tri, p.n_tris, 0, best, bi,
                                                       bestK);

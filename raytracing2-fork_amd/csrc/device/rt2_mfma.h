@@ -43,6 +43,7 @@ struct MfmaSpec {
     int tail_lanes;  // cooperative drain at <= this many live rays (pool dry)
     bool imax = false;      // max of the five terms on their bit patterns (no NaN quieting; see sweep_mfma)
     bool prefetch = false;  // the next group's records are requested before this group's products
+    bool minred = false;    // imax + one compare per group: min over the lane's 16 pairs (all one triangle)
 };
 
 // per wave: the ray fragments' staging rows (80-B stride: conflict-free
@@ -152,12 +153,13 @@ __device__ __forceinline__ float wave_max(float x) {
 
 __device__ __forceinline__ float abs_max3(const f3& v) { return fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fabsf(v.z)); }
 
-// Closest hit of every lane's ray (o, d) over all triangles; the whole wave
-// calls it (lanes without a ray of their own carry a copy of a live one).
-// Returns false (nothing done) when a ray is outside the bound's range.
+// Closest hit of every lane's ray (o, d) over the 16-triangle groups [G0, G1)
+// (all of them by default); the whole wave calls it (lanes without a ray of
+// their own carry a copy of a live one).  Returns false (nothing done) when a
+// ray is outside the bound's range.
 template <MfmaSpec S>
 __device__ __forceinline__ bool sweep_mfma(const RenderParams& p, MfmaWaveLds& sh, const f3& o, const f3& d, float& best,
-                                           int& bi, float& bestK) {
+                                           int& bi, float& bestK, int G0 = 0, int G1 = -1) {
     const int lane = (int)lane_id();
     const f3 m = cross(d, o);
     if (__ballot(!(abs_max3(o) <= 0x1p20f && abs_max3(d) <= 1.0001f))) return false;  // NaN fails too
@@ -202,25 +204,32 @@ __device__ __forceinline__ bool sweep_mfma(const RenderParams& p, MfmaWaveLds& s
     for (int R = 0; R < 4; R++) bk[R] = f4v{__builtin_inff(), __builtin_inff(), __builtin_inff(), __builtin_inff()};
 
     const h8* frag = reinterpret_cast<const h8*>(p.mfma_frag);
-    const int ng = (p.n_tris + 15) >> 4;
+    const int ng = G1 < 0 ? (p.n_tris + 15) >> 4 : G1;
     h8 b0, b1, b2, b3, b4;
     float tau;
-    auto fetch = [&](int G) {
-        const h8* fg = frag + (size_t)G * (kMfmaQ * 64) + lane;
+    // per-lane record pointers advanced in VGPRs (no per-group reload of the
+    // spilled base addresses)
+    const h8* fg = frag + (size_t)G0 * (kMfmaQ * 64) + lane;
+    const float* tg = p.mfma_tau + 16 * G0 + (lane & 15);
+    auto fetch = [&]() {
         b0 = fg[0], b1 = fg[64], b2 = fg[128], b3 = fg[192], b4 = fg[256];
-        tau = p.mfma_tau[16 * G + (lane & 15)];
+        tau = *tg;
+        fg += kMfmaQ * 64;
+        tg += 16;
     };
-    if constexpr (S.prefetch) fetch(0);
-    for (int G = 0; G < ng; G++) {
-        if constexpr (!S.prefetch) fetch(G);
+    if constexpr (S.prefetch) fetch();
+    for (int G = G0; G < ng; G++) {
+        if constexpr (!S.prefetch) fetch();
         const h8 c0 = b0, c1 = b1, c2 = b2, c3 = b3, c4 = b4;
         const float ct = tau;
-        if constexpr (S.prefetch) fetch(G + 1 < ng ? G + 1 : G);  // in flight during this group's products
+        if constexpr (S.prefetch)
+            if (G + 1 < ng) fetch();  // in flight during this group's products
         const float Tl = ct * Tw;
         const float cd = ct * Cw;
         const f4v zero = {0.0f, 0.0f, 0.0f, 0.0f};
         const f4v cdn = {cd, cd, cd, cd};
         unsigned long long M = 0;
+        int tmin = 0x7fffffff;  // minred: min over this lane's pairs of the max term
 #pragma unroll
         for (int R = 0; R < 4; R++) {
             const f4v qU = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[R], c0, zero, 0, 0, 0);
@@ -240,13 +249,17 @@ __device__ __forceinline__ bool sweep_mfma(const RenderParams& p, MfmaWaveLds& s
                     // pass or fail; no other term can be NaN (finite products).
                     const int t3 = max(max(__float_as_int(qU[i]), __float_as_int(qV[i])), __float_as_int(qX[i]));
                     const int t = max(max(t3, __float_as_int(qT[i])), __float_as_int(Y));  // two v_max3_i32
-                    M |= __ballot(t <= __float_as_int(Tl));
+                    if constexpr (S.minred)
+                        tmin = min(tmin, t);  // every pair of a lane is triangle 16G + (lane & 15)
+                    else
+                        M |= __ballot(t <= __float_as_int(Tl));
                 } else {
                     const float t = fmaxf(fmaxf(fmaxf(qU[i], qV[i]), fmaxf(qX[i], qT[i])), Y);
                     M |= __ballot(t <= Tl);
                 }
             }
         }
+        if constexpr (S.minred) M = __ballot(tmin <= __float_as_int(Tl));
         if (M) {
             // triangles of the group with a passing pair: the exact phase, in index order
             uint32_t m16 = (uint32_t)((M | M >> 16 | M >> 32 | M >> 48) & 0xffffull);

@@ -35,8 +35,8 @@ using namespace rt2d;
 #include "rt2_sweep.h"
 #include "rt2_path.h"
 #include "rt2_brute.h"
-#include "rt2_assist.h"
 #include "rt2_mfma.h"
+#include "rt2_assist.h"
 #include "rt2_bvh.h"
 #include "rt2_misc_kernels.h"
 
@@ -474,7 +474,7 @@ constexpr int kTileTris = 1024;  // 48 KiB of LDS per tile
 // A/B experiments measured in DESIGN.md ("Tried and measured") are compiled
 // only with -DRT2_EXPERIMENTS (make EXPERIMENTS=1).
 enum Kind : int {
-    K_RESIDENT = 0, K_TILED = 1, K_SMEM = 2, K_SPLIT = 3, K_ASSIST = 4, K_MFMA = 9,  // brute force
+    K_RESIDENT = 0, K_TILED = 1, K_SMEM = 2, K_SPLIT = 3, K_ASSIST = 4, K_MFMA = 9, K_MASSIST = 10,  // brute force
     K_BVH = 5, K_BVH2 = 6, K_BVH3 = 7, K_BVH4 = 8                                     // BVH (kind >= K_BVH)
 };
 struct Variant {
@@ -514,10 +514,15 @@ constexpr AssistSpec assist12_x(int coop) {
 #endif
 constexpr TiledSpec kTiledLarge{.block = 512, .group = 4, .filter = Filter::Max3};
 constexpr AssistSpec kAssist12{.waves_per_block = 12, .group = 8, .filter = Filter::Max3, .waves = 6, .coop_rays = 32};
-constexpr MfmaSpec kMfmaI{.block = 256, .waves = 2, .tail_lanes = 16, .imax = true};
+constexpr MfmaSpec kMfmaIM{.block = 256, .waves = 2, .tail_lanes = 16, .imax = true, .minred = true};
+constexpr AssistSpec kAssistM{.waves_per_block = 12, .group = 8, .filter = Filter::Max3, .waves = 3, .coop_rays = 32,
+                              .mfma = true};
+constexpr AssistSpec kAssistMM{.waves_per_block = 12, .group = 8, .filter = Filter::Max3, .waves = 3, .coop_rays = 32,
+                               .mfma = true, .minred = true};
 constexpr Bvh3Spec kBvhDefault{.block = 256, .thresh = 16, .slab = Slab::Markstein, .waves = 5, .diag = false};
 
 #ifdef RT2_EXPERIMENTS
+constexpr MfmaSpec kMfmaI{.block = 256, .waves = 2, .tail_lanes = 16, .imax = true};
 constexpr MfmaSpec kMfmaDefault{.block = 256, .waves = 2, .tail_lanes = 16};
 constexpr MfmaSpec kMfmaIP{.block = 256, .waves = 2, .tail_lanes = 16, .imax = true, .prefetch = true};
 constexpr MfmaSpec kMfmaP{.block = 256, .waves = 2, .tail_lanes = 16, .prefetch = true};
@@ -539,9 +544,12 @@ const Variant kVariants[] = {
     RT2_VARIANT(109, K_BVH4, render_bvh4<kBvhDefault>, 256, "bvh4/256/t16/w5"),           // default (BVH traversal)
     RT2_VARIANT(86, K_TILED, render_tiled<kTiledLarge>, 512, "tiled/512/max3f4"),          // > kSmemMaxTris
     RT2_VARIANT(92, K_ASSIST, render_assist<kAssist12>, 768, "assist12/max3f8/w6"),        // < 4 items per lane
-    RT2_VARIANT(131, K_MFMA, render_mfma<kMfmaI>, 256, "mfma/256/f16x3/coop16/w2/imax"),  // default (<= kMfmaMaxTris)
+    RT2_VARIANT(137, K_MFMA, render_mfma<kMfmaIM>, 256, "mfma/256/f16x3/coop16/w2/imax/minred"),  // default (<= kMfmaMaxTris)
+    RT2_VARIANT(138, K_MASSIST, render_assist<kAssistM>, 768, "massist12/f16x3/w3/imax"),
+    RT2_VARIANT(139, K_MASSIST, render_assist<kAssistMM>, 768, "massist12/f16x3/w3/imax/minred"),
     RT2_VARIANT(136, K_SMEM, render_smem<kSmemDefault>, 256, "smem/256/max3f8/coop32/w6/lockstep"),  // variant 0 forced (id 0 = automatic)
 #ifdef RT2_EXPERIMENTS
+    RT2_VARIANT(131, K_MFMA, render_mfma<kMfmaI>, 256, "mfma/256/f16x3/coop16/w2/imax"),      // a compare per pair
     RT2_VARIANT(130, K_MFMA, render_mfma<kMfmaDefault>, 256, "mfma/256/f16x3/coop16/w2"),      // f32 max (NaN quieting)
     RT2_VARIANT(132, K_MFMA, render_mfma<kMfmaIP>, 256, "mfma/256/f16x3/coop16/w2/imax/pf"),
     RT2_VARIANT(133, K_MFMA, render_mfma<kMfmaP>, 256, "mfma/256/f16x3/coop16/w2/pf"),
@@ -603,8 +611,9 @@ constexpr int kDefaultBrute = 0;
 constexpr int kDefaultBvh = 109;
 constexpr int kLargeScene = 86;  // tiled/512/max3f4: LDS tiles above kSmemMaxTris triangles
 constexpr int kSlab = 92;        // assist12/max3f8/w6: fewer than 4 items per lane (multi-GPU slabs)
-constexpr int kMfma = 131;       // mfma/256/f16x3/coop16/w2/imax: matrix-core filter (config B: 333 vs 530 ms)
-constexpr int kMfmaMaxTris = 16384;  // 5 MiB of f16 filter records: within reach of the L2s
+constexpr int kMfma = 137;       // mfma/.../imax/minred: matrix-core filter (config B: 325 vs 530 ms)
+constexpr int kMfmaMaxTris = kSmemMaxTris;  // 41 MiB of f16 records; config C (100k triangles, 480x270x2 frames
+                                           // sample): 4.9 vs 8.3 s for render_smem
 
 constexpr bool is_bvh(int kind) { return kind >= K_BVH && kind <= K_BVH4; }
 
@@ -836,7 +845,7 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     const Variant* VP = s->variant > 0 ? find_variant(s->variant) : nullptr;
     if (VP && ((s->traversal == RT2_TRAVERSAL_BVH) != is_bvh(VP->kind))) VP = nullptr;
     if (VP && VP->kind == K_RESIDENT && !fits) VP = nullptr;  // cannot hold this scene
-    if (VP && VP->kind == K_MFMA && !s->mfma_ok) VP = nullptr;  // scene outside the filter's range
+    if (VP && (VP->kind == K_MFMA || VP->kind == K_MASSIST) && !s->mfma_ok) VP = nullptr;  // scene outside the filter's range
     if (!VP && s->traversal == RT2_TRAVERSAL_BVH) VP = find_variant(kDefaultBvh);
     if (!VP) {
         int vi = s->n_tris <= kSmemMaxTris ? kDefaultBrute : kLargeScene;
@@ -852,10 +861,12 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
             int occ0 = 0;
             HIPCHECK(variant_occupancy(*W, &occ0, 0));
             const unsigned long long lanes = (unsigned long long)s->num_cus * (unsigned long long)std::max(occ0, 1) * W->block;
-            if (p.n_items < 4 * lanes)
+            if (s->mfma_ok && s->n_tris <= kMfmaMaxTris && find_variant(kMfma))
+                vi = kMfma;  // the filter on the matrix cores (rt2_mfma.h; DESIGN.md "The matrix filter"):
+                             // whole config B 331 vs 530 ms, its 1/2, 1/4, 1/8 slabs 185 / 101 / 66 ms vs
+                             // 267 / 143 / 76 for the assist kernel
+            else if (p.n_items < 4 * lanes)
                 vi = kSlab;
-            else if (s->mfma_ok && s->n_tris <= kMfmaMaxTris && find_variant(kMfma))
-                vi = kMfma;  // the filter on the matrix cores (rt2_mfma.h; DESIGN.md "The matrix filter")
         }
         VP = find_variant(vi);
     }
@@ -877,7 +888,7 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     HIPCHECK(variant_occupancy(V, &occ, lds));
     occ = std::max(occ, 1);
     unsigned long long blocks = (unsigned long long)s->num_cus * occ;
-    if (V.kind == K_ASSIST) {
+    if (V.kind == K_ASSIST || V.kind == K_MASSIST) {
         // every resident workgroup is launched: waves without items help the
         // busy waves of their workgroup.  Below 2 items per lane a quarter of
         // the waves take items (each owner has ~3 helpers; 1/4 and 1/8 slabs
@@ -886,7 +897,7 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
         const int nw = V.block / 64;
         const unsigned long long lanes = blocks * (unsigned long long)V.block;
         p.assist_cap = p.n_items < 2 * lanes ? std::max(1, nw / 4) : nw;
-        const int g = 8;  // the sweep's filter group
+        const int g = V.kind == K_MASSIST ? 16 : 8;  // the sweep's filter group (MFMA: 16-triangle record groups)
         int chunk = (s->n_tris + 2 * nw - 1) / (2 * nw);
         chunk = std::max(g, (chunk + g - 1) / g * g);
         p.assist_chunk = chunk;

@@ -12,10 +12,12 @@ from test_gpu_parity import assert_exact, oracle_mean
 
 pytestmark = pytest.mark.gpu
 
-MFMA = 131
-# product kernel (integer max of the terms); experiment build: f32 max, record
-# prefetch, 4 waves per SIMD
-VARIANTS = [131] + ([130, 132, 133, 134, 135] if EXPERIMENTS else [])
+MFMA = 137
+# product kernels: render_mfma (integer max of the terms, one compare per
+# group) and the assist kernel with the matrix filter (138, 139: forced here,
+# so every segment with helpers is posted as a job of group-range units);
+# experiment build: f32 max, a compare per pair, record prefetch, 4 waves/SIMD
+VARIANTS = [137, 138, 139] + ([130, 131, 132, 133, 134, 135] if EXPERIMENTS else [])
 
 
 @pytest.fixture(params=VARIANTS, ids=lambda v: f"v{v}")
