@@ -44,6 +44,7 @@ struct MfmaSpec {
     bool imax = false;      // max of the five terms on their bit patterns (no NaN quieting; see sweep_mfma)
     bool prefetch = false;  // the next group's records are requested before this group's products
     bool minred = false;    // imax + one compare per group: min over the lane's 16 pairs (all one triangle)
+    bool lockstep = true;   // the workgroup's waves start every segment together (one barrier per segment)
 };
 
 // per wave: the ray fragments' staging rows (80-B stride: conflict-free
@@ -298,8 +299,12 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
     for (;;) {
         advance(L, p);
         const unsigned long long act = __ballot(L.st == ST_TRACE);
-        if (!__syncthreads_or(act != 0)) break;
-        if (!act) continue;
+        if constexpr (S.lockstep) {
+            if (!__syncthreads_or(act != 0)) break;
+            if (!act) continue;
+        } else if (!act) {
+            break;
+        }
         if (__popcll(act) <= (unsigned)S.tail_lanes && __any(L.st == ST_DONE)) {
             float mybest = 1e38f;
             int mybi = -1;

@@ -109,9 +109,9 @@ def test_auto_variant_by_items_per_lane(rt2mod, config_scene, torch_cuda):
     u = rt2mod.offline_uniforms(spec.width, spec.height, spec.bounces, spec.rays, sd.num_triangles)
     scene = rt2mod.Scene(sd, 0)
     full = scene.render_host(u, 0, 1)
-    assert _last_variant(rt2mod, scene) == "mfma/256/f16x3/coop16/w2/imax/minred"
-    for n, want in ((2, "mfma/256/f16x3/coop16/w2/imax/minred"), (4, "mfma/256/f16x3/coop16/w2/imax/minred"),
-                    (8, "mfma/256/f16x3/coop16/w2/imax/minred")):
+    assert _last_variant(rt2mod, scene) == "mfma/256/f16x3/coop8/w2/imax/minred"
+    for n, want in ((2, "mfma/256/f16x3/coop8/w2/imax/minred"), (4, "mfma/256/f16x3/coop8/w2/imax/minred"),
+                    (8, "mfma/256/f16x3/coop8/w2/imax/minred")):
         sh = rt2mod.shard(1, n - 1, n)
         img = scene.render_host(u, 0, 1, sh)
         assert _last_variant(rt2mod, scene) == want
@@ -291,11 +291,11 @@ def test_frame_split_identical(rt2mod, oraclemod, config_scene, torch_cuda, trav
 
 
 # brute-force kernel variants that change the schedule, not the arithmetic:
-# the product variants (0 = automatic, 86, 92, 137, 138/139 = the assist kernel with the matrix
-# filter, 136 = the scalar path forced) and, in an experiment build, the A/B
+# the product variants (0 = automatic, 86, 92, 140 = the matrix filter, 136 = the scalar path
+# forced) and, in an experiment build, the A/B
 # variants (masked/plk filters, resident LDS, cooperative and team tail modes,
 # split waves, the round-1 slab kernels, occupancy hints)
-BRUTE_VARIANTS = [0, 86, 92, 137, 136, 138, 139] + ([22, 24, 28, 52, 64, 65, 66, 67, 68, 70, 71, 72, 73, 74, 76, 79, 80, 84, 85, 87, 89, 95, 97, 101, 104, 106,
+BRUTE_VARIANTS = [0, 86, 92, 140, 136] + ([137, 138, 139, 143, 144, 145, 146] if EXPERIMENTS else []) + ([22, 24, 28, 52, 64, 65, 66, 67, 68, 70, 71, 72, 73, 74, 76, 79, 80, 84, 85, 87, 89, 95, 97, 101, 104, 106,
                                  90] if EXPERIMENTS else [])
 
 
@@ -314,7 +314,7 @@ def test_brute_variants_bit_exact(rt2mod, oraclemod, config_scene, torch_cuda, v
     assert st.segments == segs
 
 
-@pytest.mark.parametrize("variant", [92, 138, 139] + ([71, 72, 84, 85, 90] if EXPERIMENTS else []))
+@pytest.mark.parametrize("variant", [92] + ([138, 139, 71, 72, 84, 85, 90] if EXPERIMENTS else []))
 @pytest.mark.parametrize("split_frames", [False, True])
 def test_split_waves_outputs(rt2mod, oraclemod, config_scene, torch_cuda, variant, split_frames):
     """Kernels whose waves share rays — split mode (S waves per 64 rays, one
