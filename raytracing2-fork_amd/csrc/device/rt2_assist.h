@@ -104,8 +104,9 @@ __device__ __forceinline__ void assist_unit(const RenderParams& p, AssistLds<NW,
         int bi = -1;
         const f3 ro = mk(r[0], r[64], r[128]), rd = mk(r[192], r[256], r[320]);
         bool done = false;
+        MfmaDiag dg;  // unused (assist specs count nothing)
         if constexpr (S.mfma)  // chunks are whole 16-triangle groups; posted idle lanes carry a live ray
-            done = sweep_mfma<assist_mfma_spec<S>()>(p, sh.mw[w], ro, rd, best, bi, bestK, lo >> 4, (hi + 15) >> 4);
+            done = sweep_mfma<assist_mfma_spec<S>()>(p, sh.mw[w], ro, rd, best, bi, bestK, dg, lo >> 4, (hi + 15) >> 4);
         if (!done)
             sweep_masked<S.group, true, S.filter>(ro, rd, nullptr, (const float*)p.tri + 12 * (size_t)lo, hi - lo, lo,
                                                   best, bi, bestK);
@@ -218,7 +219,8 @@ __global__ __launch_bounds__(64 * S.waves_per_block) __attribute__((amdgpu_waves
                     bi = (int)(uint32_t)key;
                 }
             } else if constexpr (S.mfma) {
-                if (!sweep_mfma<assist_mfma_spec<S>()>(p, sh.mw[w], po, pd, best, bi, bestK) && L.st == ST_TRACE)
+                MfmaDiag dg;
+                if (!sweep_mfma<assist_mfma_spec<S>()>(p, sh.mw[w], po, pd, best, bi, bestK, dg) && L.st == ST_TRACE)
                     sweep_masked<S.group, true, S.filter>(L.o, L.d, nullptr, (const float*)p.tri, p.n_tris, 0, best,
                                                           bi, bestK);
             } else if (L.st == ST_TRACE) {

@@ -45,6 +45,12 @@ struct MfmaSpec {
     bool prefetch = false;  // the next group's records are requested before this group's products
     bool minred = false;    // imax + one compare per group: min over the lane's 16 pairs (all one triangle)
     bool lockstep = true;   // the workgroup's waves start every segment together (one barrier per segment)
+    bool diag = false;      // count groups / groups with survivors / exact tests (experiment variants only)
+};
+
+// per-wave diagnostic counts of sweep_mfma (wave-uniform; MfmaSpec::diag)
+struct MfmaDiag {
+    unsigned long long groups = 0, hot = 0, exact = 0;
 };
 
 // per wave: the ray fragments' staging rows (80-B stride: conflict-free
@@ -160,7 +166,7 @@ __device__ __forceinline__ float abs_max3(const f3& v) { return fmaxf(fmaxf(fabs
 // ray is outside the bound's range.
 template <MfmaSpec S>
 __device__ __forceinline__ bool sweep_mfma(const RenderParams& p, MfmaWaveLds& sh, const f3& o, const f3& d, float& best,
-                                           int& bi, float& bestK, int G0 = 0, int G1 = -1) {
+                                           int& bi, float& bestK, MfmaDiag& dg, int G0 = 0, int G1 = -1) {
     const int lane = (int)lane_id();
     const f3 m = cross(d, o);
     if (__ballot(!(abs_max3(o) <= 0x1p20f && abs_max3(d) <= 1.0001f))) return false;  // NaN fails too
@@ -261,7 +267,9 @@ __device__ __forceinline__ bool sweep_mfma(const RenderParams& p, MfmaWaveLds& s
             }
         }
         if constexpr (S.minred) M = __ballot(tmin <= __float_as_int(Tl));
+        if constexpr (S.diag) dg.groups += 1;
         if (M) {
+            if constexpr (S.diag) dg.hot += 1;
             // triangles of the group with a passing pair: the exact phase, in index order
             uint32_t m16 = (uint32_t)((M | M >> 16 | M >> 32 | M >> 48) & 0xffffull);
             const float bk0 = bestK;
@@ -270,6 +278,7 @@ __device__ __forceinline__ bool sweep_mfma(const RenderParams& p, MfmaWaveLds& s
                 m16 &= m16 - 1;
                 const int idx = 16 * G + t;
                 if (idx >= p.n_tris) break;
+                if constexpr (S.diag) dg.exact += 1;
                 cfloat* tp = (cfloat*)p.tri + 12 * idx;
                 const MtQ q = mt_quantities(o, d, ldc4(tp), ldc4(tp + 4), ldc4(tp + 8));
                 if (mt_pass3(q, bestK)) mt_exact(q, idx, best, bi, bestK);
@@ -296,6 +305,7 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
     MfmaWaveLds& sh = wl[threadIdx.x >> 6];
     Lane L;
     lane_init(L);
+    MfmaDiag dg;
     for (;;) {
         advance(L, p);
         const unsigned long long act = __ballot(L.st == ST_TRACE);
@@ -337,7 +347,7 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
         const f3 ro = mine ? L.o : o, rd = mine ? L.d : dd;
         float best = 1e38f, bestK = 1e38f * 1.0009765625f;
         int bi = -1;
-        if (!sweep_mfma<S>(p, sh, ro, rd, best, bi, bestK) && mine)
+        if (!sweep_mfma<S>(p, sh, ro, rd, best, bi, bestK, dg) && mine)
             sweep_masked<8, true, Filter::Max3>(ro, rd, nullptr, (const float*)p.tri, p.n_tris, 0, best, bi, bestK);
         if (mine) {
             L.bounce += 1;
@@ -346,6 +356,12 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
         }
     }
     flush_counters(L, p);
+    if constexpr (S.diag)
+        if (lane_id() == 0) {
+            atomicAdd(p.seg_counter + 1, dg.groups);  // (wave, 16-triangle group) sweeps
+            atomicAdd(p.seg_counter + 2, dg.hot);     // ... with a passing pair
+            atomicAdd(p.seg_counter + 3, dg.exact);   // (wave, triangle) exact tests
+        }
 }
 
 }  // namespace

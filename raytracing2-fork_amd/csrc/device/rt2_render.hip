@@ -522,6 +522,7 @@ constexpr MfmaSpec kMfmaIM{.block = 256, .waves = 2, .tail_lanes = 16, .imax = t
 constexpr MfmaSpec kMfmaT4{.block = 256, .waves = 2, .tail_lanes = 4, .imax = true, .minred = true};
 constexpr MfmaSpec kMfmaT0{.block = 256, .waves = 2, .tail_lanes = 0, .imax = true, .minred = true};
 constexpr MfmaSpec kMfmaT8F{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true, .lockstep = false};
+constexpr MfmaSpec kMfmaT8D{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true, .diag = true};
 constexpr MfmaSpec kMfmaT4F{.block = 256, .waves = 2, .tail_lanes = 4, .imax = true, .minred = true, .lockstep = false};
 constexpr AssistSpec kAssistM{.waves_per_block = 12, .group = 8, .filter = Filter::Max3, .waves = 3, .coop_rays = 32,
                               .mfma = true};
@@ -556,6 +557,7 @@ const Variant kVariants[] = {
     RT2_VARIANT(143, K_MFMA, render_mfma<kMfmaT4>, 256, "mfma/256/f16x3/coop4/w2/imax/minred"),
     RT2_VARIANT(144, K_MFMA, render_mfma<kMfmaT0>, 256, "mfma/256/f16x3/coop0/w2/imax/minred"),
     RT2_VARIANT(145, K_MFMA, render_mfma<kMfmaT8F>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/free"),
+    RT2_VARIANT(147, K_MFMA, render_mfma<kMfmaT8D>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/diag"),  // 140 + counters
     RT2_VARIANT(146, K_MFMA, render_mfma<kMfmaT4F>, 256, "mfma/256/f16x3/coop4/w2/imax/minred/free"),
     RT2_VARIANT(138, K_MASSIST, render_assist<kAssistM>, 768, "massist12/f16x3/w3/imax"),
     RT2_VARIANT(139, K_MASSIST, render_assist<kAssistMM>, 768, "massist12/f16x3/w3/imax/minred"),
