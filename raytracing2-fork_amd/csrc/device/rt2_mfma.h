@@ -11,7 +11,11 @@
 // vector (d, m, o, 1): v_mfma_f32_16x16x32_f16 with every value split into two
 // f16 halves (x ≈ hi + lo; hi·hi + hi·lo + lo·hi in 3 of the 32 k-slots), an
 // approximation to ~2^-18 of the terms' magnitude at 16× the f32 VALU rate.
-// The VALU then only forms Y = tn + bkf·dn and the max of the five terms.
+// The distance term Y = s (tnum − bk·det) is the −tn record times a second
+// ray fragment (−(o + bk·d), −1), rebuilt when a lane's bound improves (with
+// no usable bound: (−Bmax·d, 0), the det > 0 test) — MfmaSpec::ymma, the
+// default; the older form computes dn = d·N and forms Y with one FMA per pair.
+// The VALU then only takes the max of the five terms.
 // Like the division-free filter it only decides which tests to skip: a term
 // above the threshold T implies the reference rejects ("The matrix
 // filter"), and every (wave, triangle) with a passing pair runs the exact
@@ -46,6 +50,7 @@ struct MfmaSpec {
     bool minred = false;    // imax + one compare per group: min over the lane's 16 pairs (all one triangle)
     bool lockstep = true;   // the workgroup's waves start every segment together (one barrier per segment)
     bool diag = false;      // count groups / groups with survivors / exact tests (experiment variants only)
+    bool ymma = false;      // Y = tn - bk det by a matrix product too (-tn record x ray fragment (-w, -1)): no FMA per pair
 };
 
 // per-wave diagnostic counts of sweep_mfma (wave-uniform; MfmaSpec::diag)
@@ -171,11 +176,12 @@ __device__ __forceinline__ bool sweep_mfma(const RenderParams& p, MfmaWaveLds& s
     const f3 m = cross(d, o);
     if (__ballot(!(abs_max3(o) <= 0x1p20f && abs_max3(d) <= 1.0001f))) return false;  // NaN fails too
     const float Omax = wave_max(abs_max3(o));
-    const float mx = fmaxf(fmaxf(Omax, wave_max(abs_max3(m))), 1.0f);
+    const float R0 = Omax + p.mfma_A + 1.0f;
+    float mx = fmaxf(fmaxf(Omax, wave_max(abs_max3(m))), 1.0f);
+    if constexpr (S.ymma) mx = fmaxf(mx, __builtin_fmaf(2.25f, R0, Omax));  // |o + bk d| for every bk <= Bmax
     int ex;
     (void)frexpf(mx, &ex);
     const float sigma = ldexpf(1.0f, 14 - ex);  // sigma * mx in [2^13, 2^14)
-    const float R0 = Omax + p.mfma_A + 1.0f;
     const float Tw = sigma * (kMfmaTs * R0);
     const float Cw = -kMfmaE * sigma;
     const float Bmax = kMfmaB * R0;
@@ -207,8 +213,51 @@ __device__ __forceinline__ bool sweep_mfma(const RenderParams& p, MfmaWaveLds& s
 #pragma unroll
     for (int R = 0; R < 4; R++) ra[R] = *reinterpret_cast<const h8*>(&sh.ray[16 * R + (lane & 15)][8 * (lane >> 4)]);
     f4v bk[4];
+    h8 ya[4];  // ymma: the Y fragment (-w, -1) / (-Bmax d, 0), built in the same LDS rows
+    // Y fragment of this lane's ray for its distance bound bkv: w = o + bkv d
+    // (bkv <= Bmax) with the constant slot -sigma, so that the -tn record gives
+    // Y = w.N - AN = s (tnum - bkv det); or, with no usable bound, w = Bmax d
+    // and constant 0: Y = -s Bmax det (the det > 0 test).  -w sigma as f16
+    // hi/lo in the o slots (18..26, hi lo hi like the main fragment).
+    auto build_y = [&](float bkv) {
+        const bool fin = bkv <= Bmax;
+        const float wx = fin ? __builtin_fmaf(bkv, d.x, o.x) : Bmax * d.x;
+        const float wy = fin ? __builtin_fmaf(bkv, d.y, o.y) : Bmax * d.y;
+        const float wz = fin ? __builtin_fmaf(bkv, d.z, o.z) : Bmax * d.z;
+        const float wc[3] = {wx, wy, wz};
+        _Float16 s[16];
 #pragma unroll
-    for (int R = 0; R < 4; R++) bk[R] = f4v{__builtin_inff(), __builtin_inff(), __builtin_inff(), __builtin_inff()};
+        for (int c = 0; c < 3; c++) {
+            const float v = -wc[c] * sigma;
+            const _Float16 hi = (_Float16)v;
+            const _Float16 lo = (_Float16)(v - (float)hi);
+            s[2 + 3 * c] = hi;
+            s[3 + 3 * c] = lo;
+            s[4 + 3 * c] = hi;
+        }
+        s[0] = s[1] = (_Float16)0.0f;  // slots 16, 17: d.z (zero here)
+        s[11] = s[12] = (_Float16)(fin ? -sigma : 0.0f);
+        s[13] = s[14] = s[15] = (_Float16)0.0f;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // every lane has read the rows' previous contents
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        h8* row = reinterpret_cast<h8*>(&sh.ray[lane][0]);
+        row[0] = h8{};
+        row[1] = h8{};
+        row[2] = h8{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7]};
+        row[3] = h8{s[8], s[9], s[10], s[11], s[12], s[13], s[14], s[15]};
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int R = 0; R < 4; R++) ya[R] = *reinterpret_cast<const h8*>(&sh.ray[16 * R + (lane & 15)][8 * (lane >> 4)]);
+    };
+    if constexpr (S.ymma) {
+        build_y(bestK);
+    } else {
+#pragma unroll
+        for (int R = 0; R < 4; R++) bk[R] = f4v{__builtin_inff(), __builtin_inff(), __builtin_inff(), __builtin_inff()};
+    }
 
     const h8* frag = reinterpret_cast<const h8*>(p.mfma_frag);
     const int ng = G1 < 0 ? (p.n_tris + 15) >> 4 : G1;
@@ -219,7 +268,8 @@ __device__ __forceinline__ bool sweep_mfma(const RenderParams& p, MfmaWaveLds& s
     const h8* fg = frag + (size_t)G0 * (kMfmaQ * 64) + lane;
     const float* tg = p.mfma_tau + 16 * G0 + (lane & 15);
     auto fetch = [&]() {
-        b0 = fg[0], b1 = fg[64], b2 = fg[128], b3 = fg[192], b4 = fg[256];
+        b0 = fg[0], b1 = fg[64], b2 = fg[128], b3 = fg[192];
+        if constexpr (!S.ymma) b4 = fg[256];
         tau = *tg;
         fg += kMfmaQ * 64;
         tg += 16;
@@ -227,7 +277,7 @@ __device__ __forceinline__ bool sweep_mfma(const RenderParams& p, MfmaWaveLds& s
     if constexpr (S.prefetch) fetch();
     for (int G = G0; G < ng; G++) {
         if constexpr (!S.prefetch) fetch();
-        const h8 c0 = b0, c1 = b1, c2 = b2, c3 = b3, c4 = b4;
+        const h8 c0 = b0, c1 = b1, c2 = b2, c3 = b3, c4 = S.ymma ? b3 : b4;
         const float ct = tau;
         if constexpr (S.prefetch)
             if (G + 1 < ng) fetch();  // in flight during this group's products
@@ -243,10 +293,14 @@ __device__ __forceinline__ bool sweep_mfma(const RenderParams& p, MfmaWaveLds& s
             const f4v qV = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[R], c1, zero, 0, 0, 0);
             const f4v qX = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[R], c2, zero, 0, 0, 0);
             const f4v qT = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[R], c3, zero, 0, 0, 0);
-            const f4v qD = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[R], c4, cdn, 0, 0, 0);
+            f4v qD;
+            if constexpr (S.ymma)
+                qD = __builtin_amdgcn_mfma_f32_16x16x32_f16(ya[R], c3, zero, 0, 0, 0);  // Y itself
+            else
+                qD = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[R], c4, cdn, 0, 0, 0);
 #pragma unroll
             for (int i = 0; i < 4; i++) {
-                const float Y = __builtin_fmaf(bk[R][i], qD[i], -qT[i]);
+                const float Y = S.ymma ? qD[i] : __builtin_fmaf(bk[R][i], qD[i], -qT[i]);
                 if constexpr (S.imax) {
                     // t <= Tl (Tl > 0) on the bit patterns as signed integers:
                     // negative floats are negative integers, positive floats
@@ -283,7 +337,9 @@ __device__ __forceinline__ bool sweep_mfma(const RenderParams& p, MfmaWaveLds& s
                 const MtQ q = mt_quantities(o, d, ldc4(tp), ldc4(tp + 4), ldc4(tp + 8));
                 if (mt_pass3(q, bestK)) mt_exact(q, idx, best, bi, bestK);
             }
-            if (__ballot(bestK != bk0)) {
+            if constexpr (S.ymma) {
+                if (__ballot(bestK != bk0)) build_y(bestK);
+            } else if (__ballot(bestK != bk0)) {
                 sh.bk[lane] = bestK <= Bmax ? bestK : __builtin_inff();
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();

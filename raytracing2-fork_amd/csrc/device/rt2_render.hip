@@ -514,15 +514,20 @@ constexpr AssistSpec assist12_x(int coop) {
 #endif
 constexpr TiledSpec kTiledLarge{.block = 512, .group = 4, .filter = Filter::Max3};
 constexpr AssistSpec kAssist12{.waves_per_block = 12, .group = 8, .filter = Filter::Max3, .waves = 6, .coop_rays = 32};
-constexpr MfmaSpec kMfmaT8{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true};
+constexpr MfmaSpec kMfmaT8Y{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true, .ymma = true};
 constexpr Bvh3Spec kBvhDefault{.block = 256, .thresh = 16, .slab = Slab::Markstein, .waves = 5, .diag = false};
 
 #ifdef RT2_EXPERIMENTS
+constexpr MfmaSpec kMfmaT8{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true};
 constexpr MfmaSpec kMfmaIM{.block = 256, .waves = 2, .tail_lanes = 16, .imax = true, .minred = true};
 constexpr MfmaSpec kMfmaT4{.block = 256, .waves = 2, .tail_lanes = 4, .imax = true, .minred = true};
 constexpr MfmaSpec kMfmaT0{.block = 256, .waves = 2, .tail_lanes = 0, .imax = true, .minred = true};
 constexpr MfmaSpec kMfmaT8F{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true, .lockstep = false};
 constexpr MfmaSpec kMfmaT8D{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true, .diag = true};
+constexpr MfmaSpec kMfmaT8YD{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true, .diag = true,
+                              .ymma = true};
+constexpr MfmaSpec kMfmaT8P3{.block = 256, .waves = 3, .tail_lanes = 8, .imax = true, .prefetch = true, .minred = true};
+constexpr MfmaSpec kMfmaT8P2{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .prefetch = true, .minred = true};
 constexpr MfmaSpec kMfmaT4F{.block = 256, .waves = 2, .tail_lanes = 4, .imax = true, .minred = true, .lockstep = false};
 constexpr AssistSpec kAssistM{.waves_per_block = 12, .group = 8, .filter = Filter::Max3, .waves = 3, .coop_rays = 32,
                               .mfma = true};
@@ -550,14 +555,18 @@ const Variant kVariants[] = {
     RT2_VARIANT(109, K_BVH4, render_bvh4<kBvhDefault>, 256, "bvh4/256/t16/w5"),           // default (BVH traversal)
     RT2_VARIANT(86, K_TILED, render_tiled<kTiledLarge>, 512, "tiled/512/max3f4"),          // > kSmemMaxTris
     RT2_VARIANT(92, K_ASSIST, render_assist<kAssist12>, 768, "assist12/max3f8/w6"),        // < 4 items per lane
-    RT2_VARIANT(140, K_MFMA, render_mfma<kMfmaT8>, 256, "mfma/256/f16x3/coop8/w2/imax/minred"),  // default (<= kMfmaMaxTris)
+    RT2_VARIANT(150, K_MFMA, render_mfma<kMfmaT8Y>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma"),  // default (<= kMfmaMaxTris)
     RT2_VARIANT(136, K_SMEM, render_smem<kSmemDefault>, 256, "smem/256/max3f8/coop32/w6/lockstep"),  // variant 0 forced (id 0 = automatic)
 #ifdef RT2_EXPERIMENTS
+    RT2_VARIANT(140, K_MFMA, render_mfma<kMfmaT8>, 256, "mfma/256/f16x3/coop8/w2/imax/minred"),  // Y by one FMA per pair
     RT2_VARIANT(137, K_MFMA, render_mfma<kMfmaIM>, 256, "mfma/256/f16x3/coop16/w2/imax/minred"),  // drain at 16 live rays
     RT2_VARIANT(143, K_MFMA, render_mfma<kMfmaT4>, 256, "mfma/256/f16x3/coop4/w2/imax/minred"),
     RT2_VARIANT(144, K_MFMA, render_mfma<kMfmaT0>, 256, "mfma/256/f16x3/coop0/w2/imax/minred"),
     RT2_VARIANT(145, K_MFMA, render_mfma<kMfmaT8F>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/free"),
     RT2_VARIANT(147, K_MFMA, render_mfma<kMfmaT8D>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/diag"),  // 140 + counters
+    RT2_VARIANT(151, K_MFMA, render_mfma<kMfmaT8YD>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma/diag"),
+    RT2_VARIANT(148, K_MFMA, render_mfma<kMfmaT8P3>, 256, "mfma/256/f16x3/coop8/w3/imax/minred/pf"),  // 140 + prefetch, 3 waves
+    RT2_VARIANT(149, K_MFMA, render_mfma<kMfmaT8P2>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/pf"),  // 140 + prefetch
     RT2_VARIANT(146, K_MFMA, render_mfma<kMfmaT4F>, 256, "mfma/256/f16x3/coop4/w2/imax/minred/free"),
     RT2_VARIANT(138, K_MASSIST, render_assist<kAssistM>, 768, "massist12/f16x3/w3/imax"),
     RT2_VARIANT(139, K_MASSIST, render_assist<kAssistMM>, 768, "massist12/f16x3/w3/imax/minred"),
@@ -623,7 +632,7 @@ constexpr int kDefaultBrute = 0;
 constexpr int kDefaultBvh = 109;
 constexpr int kLargeScene = 86;  // tiled/512/max3f4: LDS tiles above kSmemMaxTris triangles
 constexpr int kSlab = 92;        // assist12/max3f8/w6: fewer than 4 items per lane (multi-GPU slabs)
-constexpr int kMfma = 140;       // mfma/.../coop8/imax/minred: matrix-core filter (config B: 318 vs 530 ms)
+constexpr int kMfma = 150;       // mfma/.../coop8/imax/minred/ymma: matrix-core filter (config B: 296 vs 530 ms)
 constexpr int kMfmaMaxTris = kSmemMaxTris;  // 41 MiB of f16 records; config C (100k triangles, 480x270x2 frames
                                            // sample): 4.9 vs 8.3 s for render_smem
 

@@ -1,5 +1,5 @@
-"""Matrix-filter survivor statistics (diagnostic variant 147 = the default
-matrix kernel 140 plus counters; experiment build, RT2_LIB=exp): per
+"""Matrix-filter survivor statistics (diagnostic variants 147 / 151 = the
+matrix kernels 140 / 150 (the default) plus counters; experiment build, RT2_LIB=exp): per
 (wave, 16-triangle group) sweep, how often a pair passes the filter (the wave
 enters the exact phase) and how many (wave, triangle) exact tests follow."""
 import argparse
@@ -16,7 +16,7 @@ import rt2  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="B")
-ap.add_argument("--variants", default="140,147")
+ap.add_argument("--variants", default="150,151")
 ap.add_argument("--width", type=int, default=1920)
 ap.add_argument("--height", type=int, default=1080)
 a = ap.parse_args()

@@ -216,16 +216,18 @@ static int mfma_record(f3 a, f3 e0, f3 e1, f3 n, double slot[MQ][32], double* ta
  * As.  The accumulation of the 32 exact f16 products (+ C) in f32 is replaced
  * by the exact sum moved by the worst-case f32 summation error (31 u Σ|p|)
  * toward rejection: a pass here is a pass for any summation order. */
-static int pass_mfma(f3 o, f3 d, double slot[MQ][32], double tau, float As, float Ow, float Mw, float bestK) {
+static int pass_mfma(f3 o, f3 d, double slot[MQ][32], double tau, float As, float Ow, float Mw, float bestK,
+                     int ymma) {
     const f3 m = cross(d, o);
     const float ao = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
     const float am = fmaxf(fmaxf(fabsf(m.x), fabsf(m.y)), fabsf(m.z));
     const float Omax = fmaxf(ao, Ow);
-    const float mx = fmaxf(fmaxf(Omax, fmaxf(am, Mw)), 1.0f);
+    const float R0 = Omax + As + 1.0f;
+    float mx = fmaxf(fmaxf(Omax, fmaxf(am, Mw)), 1.0f);
+    if (ymma) mx = fmaxf(mx, fmaf(2.25f, R0, Omax));  /* |o + bk d| for any bk <= Bmax */
     int ex;
     (void)frexpf(mx, &ex);
     const float sigma = ldexpf(1.0f, 14 - ex);
-    const float R0 = Omax + As + 1.0f;
     const float Tw = sigma * (0x1p-10f * R0);
     const float Cw = -0x1p-14f * sigma;
     const float Bmax = 2.0f * R0;
@@ -252,8 +254,34 @@ static int pass_mfma(f3 o, f3 d, double slot[MQ][32], double tau, float As, floa
         qv[q] = (float)s;
         qe[q] = (float)(31.0 * 0x1p-24 * sa) + 0x1p-149f;
     }
-    const float bk = bestK <= Bmax ? bestK : INFINITY;
-    const float Y = fmaf(bk, qv[4] + qe[4], -(qv[3] - qe[3]));
+    float Y;
+    if (ymma) {
+        /* sweep_mfma<ymma>: Y is the -tn record (slot row 3) times the ray
+         * fragment (-w, -1) with w = o + bk d (bk finite), or (-Bmax d, 0)
+         * (bk = inf: Y = Bmax d.N = -s Bmax det, the sign test) */
+        const int fin = bestK <= Bmax;
+        const float w[3] = {fin ? fmaf(bestK, d.x, o.x) : Bmax * d.x, fin ? fmaf(bestK, d.y, o.y) : Bmax * d.y,
+                            fin ? fmaf(bestK, d.z, o.z) : Bmax * d.z};
+        double yr[32];
+        for (int k = 0; k < 32; k++) yr[k] = 0.0;
+        for (int c = 0; c < 3; c++) {
+            const float v = -w[c] * sigma;
+            const double hi = to_f16(v);
+            const double lo = to_f16(v - (float)hi);
+            yr[18 + 3 * c] = hi, yr[19 + 3 * c] = lo, yr[20 + 3 * c] = hi;
+        }
+        yr[27] = yr[28] = fin ? -sigma : 0.0f;
+        double sy = 0.0, sa = 0.0;
+        for (int k = 0; k < 32; k++) {
+            const double p = yr[k] * slot[3][k];
+            sy += p;
+            sa += fabs(p);
+        }
+        Y = (float)sy + ((float)(31.0 * 0x1p-24 * sa) + 0x1p-149f);
+    } else {
+        const float bk = bestK <= Bmax ? bestK : INFINITY;
+        Y = fmaf(bk, qv[4] + qe[4], -(qv[3] - qe[3]));
+    }
     const float t = fmaxf(fmaxf(fmaxf(qv[0] + qe[0], qv[1] + qe[1]), fmaxf(qv[2] + qe[2], qv[3] + qe[3])), Y);
     return t <= Tl;
 }
@@ -263,6 +291,7 @@ int main(int argc, char** argv) {
     s_rng = argc > 2 ? strtoull(argv[2], 0, 10) * 0x9E3779B97F4A7C15ull + 1 : 88172645463325252ull;
     long long accepts = 0, bad_old = 0, bad_new = 0, p_old = 0, p_new = 0, bad_plk = 0, p_plk = 0, p_plk_near = 0, p_old_near = 0;
     long long bad_mfma = 0, p_mfma = 0, n_mfma = 0, p_mfma_near = 0, n_mfma_near = 0;
+    long long bad_y = 0, p_y = 0, p_y_near = 0;
     for (long long it = 0; it < n; it++) {
         const int kind = (int)(next64() % 6);
         const int far = (next64() % 4) == 0;  /* small triangle far from the origin */
@@ -332,11 +361,14 @@ int main(int argc, char** argv) {
             const float Ow = wk == 1 ? 0x1p20f * uni() : wk == 2 ? 2.0f * scale * uni() : 0.0f;
             const float Mw = wk == 3 ? 0x1p20f * uni() : 0.0f;
             const float As = inr ? fmaxf(Am, (next64() % 3) == 0 ? 0x1p20f * uni() : 0.0f) : 0x1p20f;
-            const int fm = pass_mfma(o, d, slot, tau, As, Ow, Mw, bestK);
+            const int fm = pass_mfma(o, d, slot, tau, As, Ow, Mw, bestK, 0);
+            const int fy = pass_mfma(o, d, slot, tau, As, Ow, Mw, bestK, 1);
             n_mfma++;
             p_mfma += fm;
-            if (!far && !wide && wk == 0 && inr) n_mfma_near++, p_mfma_near += fm;
+            p_y += fy;
+            if (!far && !wide && wk == 0 && inr) n_mfma_near++, p_mfma_near += fm, p_y_near += fy;
             if (ex && !fm) bad_mfma++;
+            if (ex && !fy) bad_y++;
         }
         accepts += ex;
         if (!wide) {  /* pass counts (filter efficiency) at ordinary scales only */
@@ -346,8 +378,9 @@ int main(int argc, char** argv) {
         if (ex && !fo) bad_old++;
         if (ex && !fn) bad_new++;
     }
-    printf("%lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld\n", n, accepts, bad_old, bad_new, p_old,
-           p_new, bad_plk, p_plk, bad_mfma, p_mfma, n_mfma, p_mfma_near, n_mfma_near);
+    printf("%lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld\n", n, accepts, bad_old,
+           bad_new, p_old, p_new, bad_plk, p_plk, bad_mfma, p_mfma, n_mfma, p_mfma_near, n_mfma_near, bad_y, p_y,
+           p_y_near);
     fprintf(stderr, "near-origin draws: pass_old %lld pass_plk %lld\n", p_old_near, p_plk_near);
     return 0;
 }

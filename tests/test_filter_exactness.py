@@ -33,7 +33,16 @@ def _run_mfma(exe, n, seed):
     """(violations, passes, in-range draws, passes and draws at ordinary scales)
     of the matrix-core filter (rt2_mfma.h)."""
     out = subprocess.run([exe, str(n), str(seed)], check=True, capture_output=True, text=True).stdout
-    return tuple(map(int, out.split()))[8:]
+    return tuple(map(int, out.split()))[8:13]
+
+
+def _run_mfma_y(exe, n, seed):
+    """(violations, passes, passes at ordinary scales) of the matrix-core filter
+    whose Y term is a matrix product too (MfmaSpec::ymma), and the same three
+    figures for the FMA form, on the same draws."""
+    out = subprocess.run([exe, str(n), str(seed)], check=True, capture_output=True, text=True).stdout
+    v = tuple(map(int, out.split()))
+    return v[13:16], (v[8], v[9], v[11])
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
@@ -97,4 +106,31 @@ def test_harness_detects_a_wrong_matrix_filter(tmp_path, old, new):
     exe = str(tmp_path / "mut")
     subprocess.run(["gcc", "-O2", "-std=c11", "-ffp-contract=off", "-o", exe, str(p), "-lm"], check=True)
     bad, _, _, _, _ = _run_mfma(exe, 1_000_000, 1)
+    assert bad > 0
+
+
+@pytest.mark.parametrize("seed", [6, 7])
+def test_matrix_filter_ymma_conservative(checker, seed):
+    """sweep_mfma<ymma>: Y = tn - bk det from the -tn record and the ray
+    fragment (-(o + bk d), -1), or -Bmax det with no usable bound; no accepted
+    pair is skipped, and it skips about as much as the FMA form."""
+    (bad, passes, p_near), (bad_fma, passes_fma, p_near_fma) = _run_mfma_y(checker, 2_000_000, seed)
+    assert bad == 0 and bad_fma == 0
+    assert passes <= passes_fma * 1.05 and p_near <= p_near_fma * 1.05
+
+
+@pytest.mark.parametrize("old,new", [
+    # the distance-bound fragment without its constant slot (Y = o.N + bk d.N, AN dropped)
+    ("yr[27] = yr[28] = fin ? -sigma : 0.0f;", "yr[27] = yr[28] = 0.0f;"),
+    # the sign test with the wrong sign (Y = +s Bmax det)
+    ("fin ? fmaf(bestK, d.x, o.x) : Bmax * d.x", "fin ? fmaf(bestK, d.x, o.x) : -Bmax * d.x"),
+])
+def test_harness_detects_a_wrong_ymma_filter(tmp_path, old, new):
+    src = open(SRC).read()
+    assert old in src
+    p = tmp_path / "mut.c"
+    p.write_text(src.replace(old, new))
+    exe = str(tmp_path / "mut")
+    subprocess.run(["gcc", "-O2", "-std=c11", "-ffp-contract=off", "-o", exe, str(p), "-lm"], check=True)
+    (bad, _, _), _ = _run_mfma_y(exe, 1_000_000, 1)
     assert bad > 0

@@ -12,13 +12,13 @@ from test_gpu_parity import assert_exact, oracle_mean
 
 pytestmark = pytest.mark.gpu
 
-MFMA = 140
+MFMA = 150
 # product kernel: render_mfma (integer max of the terms, one compare per group,
 # cooperative drain at <= 8 live rays); experiment build: f32 max, a compare
 # per pair, record prefetch, 4 waves/SIMD, other drain thresholds,
 # free-running waves and the assist kernel with the matrix filter (138, 139:
 # forced here, so every segment with helpers is a job of group-range units)
-VARIANTS = [140] + ([130, 131, 132, 133, 134, 135, 137, 138, 139, 143, 144, 145, 146] if EXPERIMENTS else [])
+VARIANTS = [150] + ([130, 131, 132, 133, 134, 135, 137, 138, 139, 140, 143, 144, 145, 146, 147, 148, 149, 151] if EXPERIMENTS else [])
 
 
 @pytest.fixture(params=VARIANTS, ids=lambda v: f"v{v}")
