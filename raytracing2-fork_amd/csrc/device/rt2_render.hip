@@ -515,6 +515,7 @@ constexpr AssistSpec assist12_x(int coop) {
 constexpr TiledSpec kTiledLarge{.block = 512, .group = 4, .filter = Filter::Max3};
 constexpr AssistSpec kAssist12{.waves_per_block = 12, .group = 8, .filter = Filter::Max3, .waves = 6, .coop_rays = 32};
 constexpr MfmaSpec kMfmaT8Y{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true, .ymma = true};
+constexpr MfmaSpec kMfmaT8Y4{.block = 256, .waves = 4, .tail_lanes = 8, .imax = true, .minred = true, .ymma = true};
 constexpr Bvh3Spec kBvhDefault{.block = 256, .thresh = 16, .slab = Slab::Markstein, .waves = 5, .diag = false};
 
 #ifdef RT2_EXPERIMENTS
@@ -526,6 +527,7 @@ constexpr MfmaSpec kMfmaT8F{.block = 256, .waves = 2, .tail_lanes = 8, .imax = t
 constexpr MfmaSpec kMfmaT8D{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true, .diag = true};
 constexpr MfmaSpec kMfmaT8YD{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true, .diag = true,
                               .ymma = true};
+constexpr MfmaSpec kMfmaT8Y3{.block = 256, .waves = 3, .tail_lanes = 8, .imax = true, .minred = true, .ymma = true};
 constexpr MfmaSpec kMfmaT8P3{.block = 256, .waves = 3, .tail_lanes = 8, .imax = true, .prefetch = true, .minred = true};
 constexpr MfmaSpec kMfmaT8P2{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .prefetch = true, .minred = true};
 constexpr MfmaSpec kMfmaT4F{.block = 256, .waves = 2, .tail_lanes = 4, .imax = true, .minred = true, .lockstep = false};
@@ -555,7 +557,8 @@ const Variant kVariants[] = {
     RT2_VARIANT(109, K_BVH4, render_bvh4<kBvhDefault>, 256, "bvh4/256/t16/w5"),           // default (BVH traversal)
     RT2_VARIANT(86, K_TILED, render_tiled<kTiledLarge>, 512, "tiled/512/max3f4"),          // > kSmemMaxTris
     RT2_VARIANT(92, K_ASSIST, render_assist<kAssist12>, 768, "assist12/max3f8/w6"),        // < 4 items per lane
-    RT2_VARIANT(150, K_MFMA, render_mfma<kMfmaT8Y>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma"),  // default (<= kMfmaMaxTris)
+    RT2_VARIANT(152, K_MFMA, render_mfma<kMfmaT8Y4>, 256, "mfma/256/f16x3/coop8/w4/imax/minred/ymma"),  // default (<= kMfmaMaxTris)
+    RT2_VARIANT(150, K_MFMA, render_mfma<kMfmaT8Y>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma"),  // 1.5-3 items per lane
     RT2_VARIANT(136, K_SMEM, render_smem<kSmemDefault>, 256, "smem/256/max3f8/coop32/w6/lockstep"),  // variant 0 forced (id 0 = automatic)
 #ifdef RT2_EXPERIMENTS
     RT2_VARIANT(140, K_MFMA, render_mfma<kMfmaT8>, 256, "mfma/256/f16x3/coop8/w2/imax/minred"),  // Y by one FMA per pair
@@ -565,6 +568,7 @@ const Variant kVariants[] = {
     RT2_VARIANT(145, K_MFMA, render_mfma<kMfmaT8F>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/free"),
     RT2_VARIANT(147, K_MFMA, render_mfma<kMfmaT8D>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/diag"),  // 140 + counters
     RT2_VARIANT(151, K_MFMA, render_mfma<kMfmaT8YD>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma/diag"),
+    RT2_VARIANT(153, K_MFMA, render_mfma<kMfmaT8Y3>, 256, "mfma/256/f16x3/coop8/w3/imax/minred/ymma"),
     RT2_VARIANT(148, K_MFMA, render_mfma<kMfmaT8P3>, 256, "mfma/256/f16x3/coop8/w3/imax/minred/pf"),  // 140 + prefetch, 3 waves
     RT2_VARIANT(149, K_MFMA, render_mfma<kMfmaT8P2>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/pf"),  // 140 + prefetch
     RT2_VARIANT(146, K_MFMA, render_mfma<kMfmaT4F>, 256, "mfma/256/f16x3/coop4/w2/imax/minred/free"),
@@ -632,7 +636,8 @@ constexpr int kDefaultBrute = 0;
 constexpr int kDefaultBvh = 109;
 constexpr int kLargeScene = 86;  // tiled/512/max3f4: LDS tiles above kSmemMaxTris triangles
 constexpr int kSlab = 92;        // assist12/max3f8/w6: fewer than 4 items per lane (multi-GPU slabs)
-constexpr int kMfma = 150;       // mfma/.../coop8/imax/minred/ymma: matrix-core filter (config B: 296 vs 530 ms)
+constexpr int kMfma = 152;       // mfma/.../coop8/w4/imax/minred/ymma: matrix-core filter (config B: 287 vs 530 ms)
+constexpr int kMfmaMid = 150;    // the same at 3 waves per SIMD (1.5 to 3 items per 4-wave lane)
 constexpr int kMfmaMaxTris = kSmemMaxTris;  // 41 MiB of f16 records; config C (100k triangles, 480x270x2 frames
                                            // sample): 4.9 vs 8.3 s for render_smem
 
@@ -882,11 +887,17 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
             int occ0 = 0;
             HIPCHECK(variant_occupancy(*W, &occ0, 0));
             const unsigned long long lanes = (unsigned long long)s->num_cus * (unsigned long long)std::max(occ0, 1) * W->block;
-            if (s->mfma_ok && s->n_tris <= kMfmaMaxTris && find_variant(kMfma))
-                vi = kMfma;  // the filter on the matrix cores (rt2_mfma.h; DESIGN.md "The matrix filter"):
-                             // whole config B 331 vs 530 ms, its 1/2, 1/4, 1/8 slabs 185 / 101 / 66 ms vs
-                             // 267 / 143 / 76 for the assist kernel
-            else if (p.n_items < 4 * lanes)
+            if (s->mfma_ok && s->n_tris <= kMfmaMaxTris && find_variant(kMfma) && find_variant(kMfmaMid)) {
+                // the filter on the matrix cores (rt2_mfma.h; DESIGN.md "The matrix filter"): whole
+                // config B 287 vs 530 ms, its 1/2, 1/4, 1/8 slabs 154 / 80 / 43 ms vs 267 / 143 / 76 for
+                // the assist kernel.  4 waves per SIMD, except at 1.5 to 3 items per 4-wave lane (the
+                // 1/4 slab: 1.98), where the 3-wave build's last round is fuller (80 vs 83 ms)
+                int occ4 = 0;
+                HIPCHECK(variant_occupancy(*find_variant(kMfma), &occ4, 0));
+                const double ipl = (double)p.n_items /
+                                   ((double)s->num_cus * (double)std::max(occ4, 1) * find_variant(kMfma)->block);
+                vi = (ipl >= 1.5 && ipl < 3.0) ? kMfmaMid : kMfma;
+            } else if (p.n_items < 4 * lanes)
                 vi = kSlab;
         }
         VP = find_variant(vi);
