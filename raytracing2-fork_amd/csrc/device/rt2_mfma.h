@@ -51,6 +51,7 @@ struct MfmaSpec {
     bool lockstep = true;   // the workgroup's waves start every segment together (one barrier per segment)
     bool diag = false;      // count groups / groups with survivors / exact tests (experiment variants only)
     bool ymma = false;      // Y = tn - bk det by a matrix product too (-tn record x ray fragment (-w, -1)): no FMA per pair
+    int tshift = 10;        // T = 2^-tshift (Omax + A + 1)
 };
 
 // per-wave diagnostic counts of sweep_mfma (wave-uniform; MfmaSpec::diag)
@@ -182,7 +183,7 @@ __device__ __forceinline__ bool sweep_mfma(const RenderParams& p, MfmaWaveLds& s
     int ex;
     (void)frexpf(mx, &ex);
     const float sigma = ldexpf(1.0f, 14 - ex);  // sigma * mx in [2^13, 2^14)
-    const float Tw = sigma * (kMfmaTs * R0);
+    const float Tw = sigma * (ldexpf(kMfmaTs, 10 - S.tshift) * R0);
     const float Cw = -kMfmaE * sigma;
     const float Bmax = kMfmaB * R0;
 

@@ -528,6 +528,12 @@ constexpr MfmaSpec kMfmaT8D{.block = 256, .waves = 2, .tail_lanes = 8, .imax = t
 constexpr MfmaSpec kMfmaT8YD{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true, .diag = true,
                               .ymma = true};
 constexpr MfmaSpec kMfmaT8Y3{.block = 256, .waves = 3, .tail_lanes = 8, .imax = true, .minred = true, .ymma = true};
+constexpr MfmaSpec kMfmaT8Y4T12{.block = 256, .waves = 4, .tail_lanes = 8, .imax = true, .minred = true, .ymma = true,
+                                 .tshift = 12};
+constexpr MfmaSpec kMfmaT8Y4T14{.block = 256, .waves = 4, .tail_lanes = 8, .imax = true, .minred = true, .ymma = true,
+                                 .tshift = 14};
+constexpr MfmaSpec kMfmaT8YDT12{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true, .diag = true,
+                                 .ymma = true, .tshift = 12};
 constexpr MfmaSpec kMfmaT8P3{.block = 256, .waves = 3, .tail_lanes = 8, .imax = true, .prefetch = true, .minred = true};
 constexpr MfmaSpec kMfmaT8P2{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .prefetch = true, .minred = true};
 constexpr MfmaSpec kMfmaT4F{.block = 256, .waves = 2, .tail_lanes = 4, .imax = true, .minred = true, .lockstep = false};
@@ -569,6 +575,9 @@ const Variant kVariants[] = {
     RT2_VARIANT(147, K_MFMA, render_mfma<kMfmaT8D>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/diag"),  // 140 + counters
     RT2_VARIANT(151, K_MFMA, render_mfma<kMfmaT8YD>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma/diag"),
     RT2_VARIANT(153, K_MFMA, render_mfma<kMfmaT8Y3>, 256, "mfma/256/f16x3/coop8/w3/imax/minred/ymma"),
+    RT2_VARIANT(154, K_MFMA, render_mfma<kMfmaT8Y4T12>, 256, "mfma/256/f16x3/coop8/w4/imax/minred/ymma/t12"),  // T = 2^-12 R0
+    RT2_VARIANT(155, K_MFMA, render_mfma<kMfmaT8Y4T14>, 256, "mfma/256/f16x3/coop8/w4/imax/minred/ymma/t14"),
+    RT2_VARIANT(156, K_MFMA, render_mfma<kMfmaT8YDT12>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma/t12/diag"),
     RT2_VARIANT(148, K_MFMA, render_mfma<kMfmaT8P3>, 256, "mfma/256/f16x3/coop8/w3/imax/minred/pf"),  // 140 + prefetch, 3 waves
     RT2_VARIANT(149, K_MFMA, render_mfma<kMfmaT8P2>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/pf"),  // 140 + prefetch
     RT2_VARIANT(146, K_MFMA, render_mfma<kMfmaT4F>, 256, "mfma/256/f16x3/coop4/w2/imax/minred/free"),
