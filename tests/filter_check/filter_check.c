@@ -216,8 +216,13 @@ static int mfma_record(f3 a, f3 e0, f3 e1, f3 n, double slot[MQ][32], double* ta
  * As.  The accumulation of the 32 exact f16 products (+ C) in f32 is replaced
  * by the exact sum moved by the worst-case f32 summation error (31 u Σ|p|)
  * toward rejection: a pass here is a pass for any summation order. */
+/* the threshold of the Y-by-matrix-product form (rt2_mfma.h MfmaSpec::tshift
+ * of the product variants), T = YMMA_TS (Omax + A + 1) */
+#ifndef YMMA_TS
+#define YMMA_TS 0x1p-10f
+#endif
 static int pass_mfma(f3 o, f3 d, double slot[MQ][32], double tau, float As, float Ow, float Mw, float bestK,
-                     int ymma) {
+                     int ymma, float ts) {
     const f3 m = cross(d, o);
     const float ao = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
     const float am = fmaxf(fmaxf(fabsf(m.x), fabsf(m.y)), fabsf(m.z));
@@ -228,7 +233,7 @@ static int pass_mfma(f3 o, f3 d, double slot[MQ][32], double tau, float As, floa
     int ex;
     (void)frexpf(mx, &ex);
     const float sigma = ldexpf(1.0f, 14 - ex);
-    const float Tw = sigma * (0x1p-10f * R0);
+    const float Tw = sigma * (ts * R0);
     const float Cw = -0x1p-14f * sigma;
     const float Bmax = 2.0f * R0;
     const float comp[9] = {d.x, d.y, d.z, m.x, m.y, m.z, o.x, o.y, o.z};
@@ -361,8 +366,8 @@ int main(int argc, char** argv) {
             const float Ow = wk == 1 ? 0x1p20f * uni() : wk == 2 ? 2.0f * scale * uni() : 0.0f;
             const float Mw = wk == 3 ? 0x1p20f * uni() : 0.0f;
             const float As = inr ? fmaxf(Am, (next64() % 3) == 0 ? 0x1p20f * uni() : 0.0f) : 0x1p20f;
-            const int fm = pass_mfma(o, d, slot, tau, As, Ow, Mw, bestK, 0);
-            const int fy = pass_mfma(o, d, slot, tau, As, Ow, Mw, bestK, 1);
+            const int fm = pass_mfma(o, d, slot, tau, As, Ow, Mw, bestK, 0, 0x1p-10f);
+            const int fy = pass_mfma(o, d, slot, tau, As, Ow, Mw, bestK, 1, YMMA_TS);
             n_mfma++;
             p_mfma += fm;
             p_y += fy;

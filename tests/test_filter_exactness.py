@@ -95,7 +95,7 @@ def test_matrix_filter_conservative(checker, seed):
 
 
 @pytest.mark.parametrize("old,new", [
-    ("const float Tw = sigma * (0x1p-10f * R0);", "const float Tw = sigma * (0x1p-20f * R0);"),  # margin too thin
+    ("const float Tw = sigma * (ts * R0);", "const float Tw = sigma * (ts * 0x1p-10f * R0);"),  # margin too thin
     ("const float Cw = -0x1p-14f * sigma;", "const float Cw = 0x1p-14f * sigma;"),  # det bias the wrong way
 ])
 def test_harness_detects_a_wrong_matrix_filter(tmp_path, old, new):
