@@ -51,7 +51,7 @@ struct MfmaSpec {
     bool lockstep = true;   // the workgroup's waves start every segment together (one barrier per segment)
     bool diag = false;      // count groups / groups with survivors / exact tests (experiment variants only)
     bool ymma = false;      // Y = tn - bk det by a matrix product too (-tn record x ray fragment (-w, -1)): no FMA per pair
-    int tshift = 10;        // T = 2^-tshift (Omax + A + 1)
+    int tshift = 10;        // T = 2^-tshift (Omax + A + 1); 12 for the ymma product variants
 };
 
 // per-wave diagnostic counts of sweep_mfma (wave-uniform; MfmaSpec::diag)

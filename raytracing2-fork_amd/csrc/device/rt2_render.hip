@@ -514,8 +514,10 @@ constexpr AssistSpec assist12_x(int coop) {
 #endif
 constexpr TiledSpec kTiledLarge{.block = 512, .group = 4, .filter = Filter::Max3};
 constexpr AssistSpec kAssist12{.waves_per_block = 12, .group = 8, .filter = Filter::Max3, .waves = 6, .coop_rays = 32};
-constexpr MfmaSpec kMfmaT8Y{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true, .ymma = true};
-constexpr MfmaSpec kMfmaT8Y4{.block = 256, .waves = 4, .tail_lanes = 8, .imax = true, .minred = true, .ymma = true};
+constexpr MfmaSpec kMfmaT8Y{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true, .ymma = true,
+                            .tshift = 12};
+constexpr MfmaSpec kMfmaT8Y4{.block = 256, .waves = 4, .tail_lanes = 8, .imax = true, .minred = true, .ymma = true,
+                             .tshift = 12};
 constexpr Bvh3Spec kBvhDefault{.block = 256, .thresh = 16, .slab = Slab::Markstein, .waves = 5, .diag = false};
 
 #ifdef RT2_EXPERIMENTS
@@ -528,8 +530,7 @@ constexpr MfmaSpec kMfmaT8D{.block = 256, .waves = 2, .tail_lanes = 8, .imax = t
 constexpr MfmaSpec kMfmaT8YD{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true, .diag = true,
                               .ymma = true};
 constexpr MfmaSpec kMfmaT8Y3{.block = 256, .waves = 3, .tail_lanes = 8, .imax = true, .minred = true, .ymma = true};
-constexpr MfmaSpec kMfmaT8Y4T12{.block = 256, .waves = 4, .tail_lanes = 8, .imax = true, .minred = true, .ymma = true,
-                                 .tshift = 12};
+constexpr MfmaSpec kMfmaT8Y4T10{.block = 256, .waves = 4, .tail_lanes = 8, .imax = true, .minred = true, .ymma = true};
 constexpr MfmaSpec kMfmaT8Y4T14{.block = 256, .waves = 4, .tail_lanes = 8, .imax = true, .minred = true, .ymma = true,
                                  .tshift = 14};
 constexpr MfmaSpec kMfmaT8YDT12{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true, .diag = true,
@@ -563,8 +564,8 @@ const Variant kVariants[] = {
     RT2_VARIANT(109, K_BVH4, render_bvh4<kBvhDefault>, 256, "bvh4/256/t16/w5"),           // default (BVH traversal)
     RT2_VARIANT(86, K_TILED, render_tiled<kTiledLarge>, 512, "tiled/512/max3f4"),          // > kSmemMaxTris
     RT2_VARIANT(92, K_ASSIST, render_assist<kAssist12>, 768, "assist12/max3f8/w6"),        // < 4 items per lane
-    RT2_VARIANT(152, K_MFMA, render_mfma<kMfmaT8Y4>, 256, "mfma/256/f16x3/coop8/w4/imax/minred/ymma"),  // default (<= kMfmaMaxTris)
-    RT2_VARIANT(150, K_MFMA, render_mfma<kMfmaT8Y>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma"),  // 1.5-3 items per lane
+    RT2_VARIANT(152, K_MFMA, render_mfma<kMfmaT8Y4>, 256, "mfma/256/f16x3/coop8/w4/imax/minred/ymma/t12"),  // default (<= kMfmaMaxTris)
+    RT2_VARIANT(150, K_MFMA, render_mfma<kMfmaT8Y>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma/t12"),  // 1.5-3 items per lane
     RT2_VARIANT(136, K_SMEM, render_smem<kSmemDefault>, 256, "smem/256/max3f8/coop32/w6/lockstep"),  // variant 0 forced (id 0 = automatic)
 #ifdef RT2_EXPERIMENTS
     RT2_VARIANT(140, K_MFMA, render_mfma<kMfmaT8>, 256, "mfma/256/f16x3/coop8/w2/imax/minred"),  // Y by one FMA per pair
@@ -575,8 +576,8 @@ const Variant kVariants[] = {
     RT2_VARIANT(147, K_MFMA, render_mfma<kMfmaT8D>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/diag"),  // 140 + counters
     RT2_VARIANT(151, K_MFMA, render_mfma<kMfmaT8YD>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma/diag"),
     RT2_VARIANT(153, K_MFMA, render_mfma<kMfmaT8Y3>, 256, "mfma/256/f16x3/coop8/w3/imax/minred/ymma"),
-    RT2_VARIANT(154, K_MFMA, render_mfma<kMfmaT8Y4T12>, 256, "mfma/256/f16x3/coop8/w4/imax/minred/ymma/t12"),  // T = 2^-12 R0
-    RT2_VARIANT(155, K_MFMA, render_mfma<kMfmaT8Y4T14>, 256, "mfma/256/f16x3/coop8/w4/imax/minred/ymma/t14"),
+    RT2_VARIANT(154, K_MFMA, render_mfma<kMfmaT8Y4T10>, 256, "mfma/256/f16x3/coop8/w4/imax/minred/ymma/t10"),  // T = 2^-10 R0
+    RT2_VARIANT(155, K_MFMA, render_mfma<kMfmaT8Y4T14>, 256, "mfma/256/f16x3/coop8/w4/imax/minred/ymma/t14"),  // below the proven margin
     RT2_VARIANT(156, K_MFMA, render_mfma<kMfmaT8YDT12>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma/t12/diag"),
     RT2_VARIANT(148, K_MFMA, render_mfma<kMfmaT8P3>, 256, "mfma/256/f16x3/coop8/w3/imax/minred/pf"),  // 140 + prefetch, 3 waves
     RT2_VARIANT(149, K_MFMA, render_mfma<kMfmaT8P2>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/pf"),  // 140 + prefetch

@@ -219,7 +219,7 @@ static int mfma_record(f3 a, f3 e0, f3 e1, f3 n, double slot[MQ][32], double* ta
 /* the threshold of the Y-by-matrix-product form (rt2_mfma.h MfmaSpec::tshift
  * of the product variants), T = YMMA_TS (Omax + A + 1) */
 #ifndef YMMA_TS
-#define YMMA_TS 0x1p-10f
+#define YMMA_TS 0x1p-12f
 #endif
 static int pass_mfma(f3 o, f3 d, double slot[MQ][32], double tau, float As, float Ow, float Mw, float bestK,
                      int ymma, float ts) {

@@ -100,8 +100,8 @@ def _last_variant(rt2mod, scene):
     return rt2mod.lib().rt2_variant_name(lv.value).decode()
 
 
-AUTO_MFMA = "mfma/256/f16x3/coop8/w4/imax/minred/ymma"  # variant 152 (4 waves per SIMD)
-AUTO_MFMA_MID = "mfma/256/f16x3/coop8/w2/imax/minred/ymma"  # variant 150: 1.5-3 items per 4-wave lane
+AUTO_MFMA = "mfma/256/f16x3/coop8/w4/imax/minred/ymma/t12"  # variant 152 (4 waves per SIMD)
+AUTO_MFMA_MID = "mfma/256/f16x3/coop8/w2/imax/minred/ymma/t12"  # variant 150: 1.5-3 items per 4-wave lane
 
 
 def test_auto_variant_by_items_per_lane(rt2mod, config_scene, torch_cuda):
