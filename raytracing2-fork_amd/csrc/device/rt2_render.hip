@@ -647,7 +647,8 @@ constexpr int kDefaultBvh = 109;
 constexpr int kLargeScene = 86;  // tiled/512/max3f4: LDS tiles above kSmemMaxTris triangles
 constexpr int kSlab = 92;        // assist12/max3f8/w6: fewer than 4 items per lane (multi-GPU slabs)
 constexpr int kMfma = 152;       // mfma/.../coop8/w4/imax/minred/ymma: matrix-core filter (config B: 287 vs 530 ms)
-constexpr int kMfmaMid = 150;    // the same at 3 waves per SIMD (1.5 to 3 items per 4-wave lane)
+constexpr int kMfmaMid = 150;    // the same at 3 waves per SIMD (1.5 to 3 items per 4-wave lane; large scenes)
+constexpr int kMfma4MaxTris = 8192;  // 4 waves only while the records (5 KiB per 16 triangles) fit an XCD's L2
 constexpr int kMfmaMaxTris = kSmemMaxTris;  // 41 MiB of f16 records; config C (100k triangles, 480x270x2 frames
                                            // sample): 4.9 vs 8.3 s for render_smem
 
@@ -899,14 +900,16 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
             const unsigned long long lanes = (unsigned long long)s->num_cus * (unsigned long long)std::max(occ0, 1) * W->block;
             if (s->mfma_ok && s->n_tris <= kMfmaMaxTris && find_variant(kMfma) && find_variant(kMfmaMid)) {
                 // the filter on the matrix cores (rt2_mfma.h; DESIGN.md "The matrix filter"): whole
-                // config B 287 vs 530 ms, its 1/2, 1/4, 1/8 slabs 154 / 80 / 43 ms vs 267 / 143 / 76 for
-                // the assist kernel.  4 waves per SIMD, except at 1.5 to 3 items per 4-wave lane (the
-                // 1/4 slab: 1.98), where the 3-wave build's last round is fuller (80 vs 83 ms)
+                // config B 276 vs 530 ms, its 1/2, 1/4, 1/8 slabs 152 / 77 / 42 ms vs 267 / 143 / 76 for
+                // the assist kernel.  4 waves per SIMD while the records stay in an XCD's L2, except at
+                // 1.5 to 3 items per 4-wave lane (the 1/4 slab: 1.98), where the 3-wave build's last
+                // round is fuller (80 vs 83 ms); 3 waves for larger scenes, whose records stream from
+                // the MALL (config C sample: 2.39 vs 3.02 s)
                 int occ4 = 0;
                 HIPCHECK(variant_occupancy(*find_variant(kMfma), &occ4, 0));
                 const double ipl = (double)p.n_items /
                                    ((double)s->num_cus * (double)std::max(occ4, 1) * find_variant(kMfma)->block);
-                vi = (ipl >= 1.5 && ipl < 3.0) ? kMfmaMid : kMfma;
+                vi = (s->n_tris > kMfma4MaxTris || (ipl >= 1.5 && ipl < 3.0)) ? kMfmaMid : kMfma;
             } else if (p.n_items < 4 * lanes)
                 vi = kSlab;
         }

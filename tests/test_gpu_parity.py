@@ -104,6 +104,17 @@ AUTO_MFMA = "mfma/256/f16x3/coop8/w4/imax/minred/ymma/t12"  # variant 152 (4 wav
 AUTO_MFMA_MID = "mfma/256/f16x3/coop8/w2/imax/minred/ymma/t12"  # variant 150: 1.5-3 items per 4-wave lane
 
 
+def test_auto_variant_large_scene(rt2mod, config_scene, torch_cuda):
+    """Scenes whose matrix-filter records outgrow an XCD's L2 (config C: 100k
+    triangles, 31 MB) run the 3-wave build whatever the items per lane
+    (config C sample: 2.39 vs 3.02 s at 4 waves)."""
+    sd, spec = config_scene("C")
+    u = rt2mod.offline_uniforms(64, 36, spec.bounces, 1, sd.num_triangles)
+    scene = rt2mod.Scene(sd, 0)
+    scene.render_host(u, 0, 1)
+    assert _last_variant(rt2mod, scene) == AUTO_MFMA_MID
+
+
 def test_auto_variant_by_items_per_lane(rt2mod, config_scene, torch_cuda):
     """The launcher picks the matrix-core filter kernel for the full config B
     image and for its 1/2, 1/4 and 1/8 slabs (the assist
