@@ -52,6 +52,7 @@ struct MfmaSpec {
     bool diag = false;      // count groups / groups with survivors / exact tests (experiment variants only)
     bool ymma = false;      // Y = tn - bk det by a matrix product too (-tn record x ray fragment (-w, -1)): no FMA per pair
     int tshift = 10;        // T = 2^-tshift (Omax + A + 1); 12 for the ymma product variants
+    int lds_pad = 0;        // extra static LDS per workgroup (bytes): caps the resident workgroups (experiments)
 };
 
 // per-wave diagnostic counts of sweep_mfma (wave-uniform; MfmaSpec::diag)
@@ -360,6 +361,10 @@ template <MfmaSpec S>
 __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves))) void render_mfma(RenderParams p) {
     __shared__ MfmaWaveLds wl[S.block / 64];
     MfmaWaveLds& sh = wl[threadIdx.x >> 6];
+    if constexpr (S.lds_pad > 0) {
+        __shared__ uint32_t pad[S.lds_pad / 4];
+        if (p.n_items == 0) pad[threadIdx.x] = 0;  // never taken at launch; keeps the allocation
+    }
     Lane L;
     lane_init(L);
     MfmaDiag dg;

@@ -535,6 +535,10 @@ constexpr MfmaSpec kMfmaT8Y4T14{.block = 256, .waves = 4, .tail_lanes = 8, .imax
                                  .tshift = 14};
 constexpr MfmaSpec kMfmaT8YDT12{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true, .diag = true,
                                  .ymma = true, .tshift = 12};
+constexpr MfmaSpec kMfmaT8Y2W{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true, .ymma = true,
+                               .tshift = 12, .lds_pad = 36864};  // 2 workgroups per CU: 2 waves per SIMD
+constexpr MfmaSpec kMfmaT8Y1W{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true, .ymma = true,
+                               .tshift = 12, .lds_pad = 69632};  // 1 workgroup per CU
 constexpr MfmaSpec kMfmaT8P3{.block = 256, .waves = 3, .tail_lanes = 8, .imax = true, .prefetch = true, .minred = true};
 constexpr MfmaSpec kMfmaT8P2{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .prefetch = true, .minred = true};
 constexpr MfmaSpec kMfmaT4F{.block = 256, .waves = 2, .tail_lanes = 4, .imax = true, .minred = true, .lockstep = false};
@@ -579,6 +583,8 @@ const Variant kVariants[] = {
     RT2_VARIANT(154, K_MFMA, render_mfma<kMfmaT8Y4T10>, 256, "mfma/256/f16x3/coop8/w4/imax/minred/ymma/t10"),  // T = 2^-10 R0
     RT2_VARIANT(155, K_MFMA, render_mfma<kMfmaT8Y4T14>, 256, "mfma/256/f16x3/coop8/w4/imax/minred/ymma/t14"),  // below the proven margin
     RT2_VARIANT(156, K_MFMA, render_mfma<kMfmaT8YDT12>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma/t12/diag"),
+    RT2_VARIANT(157, K_MFMA, render_mfma<kMfmaT8Y2W>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma/t12/occ2"),
+    RT2_VARIANT(158, K_MFMA, render_mfma<kMfmaT8Y1W>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma/t12/occ1"),
     RT2_VARIANT(148, K_MFMA, render_mfma<kMfmaT8P3>, 256, "mfma/256/f16x3/coop8/w3/imax/minred/pf"),  // 140 + prefetch, 3 waves
     RT2_VARIANT(149, K_MFMA, render_mfma<kMfmaT8P2>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/pf"),  // 140 + prefetch
     RT2_VARIANT(146, K_MFMA, render_mfma<kMfmaT4F>, 256, "mfma/256/f16x3/coop4/w2/imax/minred/free"),
