@@ -36,6 +36,9 @@ using namespace rt2d;
 #include "rt2_path.h"
 #include "rt2_brute.h"
 #include "rt2_mfma.h"
+#ifdef RT2_EXPERIMENTS
+#include "rt2_mfma32.h"
+#endif
 #include "rt2_assist.h"
 #include "rt2_bvh.h"
 #include "rt2_misc_kernels.h"
@@ -583,6 +586,7 @@ const Variant kVariants[] = {
     RT2_VARIANT(154, K_MFMA, render_mfma<kMfmaT8Y4T10>, 256, "mfma/256/f16x3/coop8/w4/imax/minred/ymma/t10"),  // T = 2^-10 R0
     RT2_VARIANT(155, K_MFMA, render_mfma<kMfmaT8Y4T14>, 256, "mfma/256/f16x3/coop8/w4/imax/minred/ymma/t14"),  // below the proven margin
     RT2_VARIANT(156, K_MFMA, render_mfma<kMfmaT8YDT12>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma/t12/diag"),
+    RT2_VARIANT(159, K_MFMA, render_mfma32<kMfmaT8Y>, 256, "mfma32/256/f16x3/coop8/w2/imax/minred/ymma/t12"),  // 32x32x16
     RT2_VARIANT(157, K_MFMA, render_mfma<kMfmaT8Y2W>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma/t12/occ2"),
     RT2_VARIANT(158, K_MFMA, render_mfma<kMfmaT8Y1W>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma/t12/occ1"),
     RT2_VARIANT(148, K_MFMA, render_mfma<kMfmaT8P3>, 256, "mfma/256/f16x3/coop8/w3/imax/minred/pf"),  // 140 + prefetch, 3 waves
