@@ -4,13 +4,16 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config B] [--traversal brute|bvh]
                     [--no-cpu-baseline] [--no-alt] [--no-config-c]
 
+--gpus N > 1 without a launcher starts N ranks itself (torch.distributed.run,
+one process per GPU, master 127.0.0.1); under a launcher WORLD_SIZE must equal N.
+
 One "step" = one render of the configuration's image (config B: campfire +
 Cornell box, 1920x1080, 64 rays/pixel x 1 frame, 8 bounces) —
 rt2_render into a device accumulator + the device resolve (+ one RCCL gather of
 the framebuffer to rank 0 for N > 1; rows interleaved across ranks, so the
 image is fixed as N grows: strong scaling).  Inputs (scene arrays) are
-uploaded to HBM before the timed region.  For N > 1 the driver launches one
-process per GPU through torch.distributed.run.
+uploaded to HBM before the timed region.  For N > 1 one process per GPU runs
+under torch.distributed.run (the driver's launch, or bench.py's own).
 
 Prints ONE JSON line (rank 0):
   value         Msamples/s of the whole job = W*H*R*F*K / max-over-ranks wall time
@@ -75,7 +78,65 @@ def parse():
     ap.add_argument("--no-alt", action="store_true", help="skip timing the other traversal beside the headline")
     ap.add_argument("--no-config-c", action="store_true", help="skip the config C (north-star target) leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target seconds per CPU baseline mode")
+    ap.add_argument("--plumbing", action="store_true",
+                    help="launch/collective path only, no GPU (CPU tests of --gpus N): each rank gathers a synthetic "
+                         "slab of its image rows and rank 0 checks the assembled image")
     return ap.parse_args()
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def ensure_world(args):
+    """`--gpus N` on its own: with no launcher (WORLD_SIZE unset) and N > 1, start
+    one fresh process per GPU through torch.distributed.run (master 127.0.0.1)
+    and exit with its status — this process has made no GPU call (torch is not
+    even imported yet), so nothing is inherited or exec'd from a GPU-initialised
+    process.  Under a launcher, WORLD_SIZE must equal --gpus."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks",
+                  file=sys.stderr)
+            sys.exit(2)
+        return
+    if args.gpus <= 1:
+        return
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
+
+
+def plumbing(args, world, rank):
+    """The N-rank launch + gather path without a GPU: rank r's slab holds its own
+    image rows (value = row index), gathered to rank 0 and checked there."""
+    import torch
+    import torch.distributed as dist
+    from rt2 import dist as rdist
+    H, W = 64, 8
+    ids = rdist.slab_row_ids(H, args.tile_rows, rank, world)
+    slab = torch.as_tensor(ids, dtype=torch.float32)[:, None, None].expand(len(ids), W, 4).contiguous()
+    t0 = time.perf_counter()
+    img = rdist.gather_image(slab, H, W, args.tile_rows, rank, world) if world > 1 else slab
+    dist.barrier() if world > 1 else None
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        ok = bool((img[:, :, 0] == torch.arange(H, dtype=torch.float32)[:, None]).all())
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "Msamples/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "plumbing": True, "gather_ok": ok,
+                          "ms_per_step": round(float(el[0]) * 1e3, 3), "higher_is_better": True,
+                          "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+                          "config": {"workload": "plumbing: row-tile gather of a 64x8 synthetic image",
+                                     "parallelism": f"row-tile x{world}" if world > 1 else "1 GPU"}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 # Device sources the brute-force and BVH render kernels are compiled from (one
@@ -347,6 +408,7 @@ def config_c_leg(torch, rt2, stream, threads, host, seconds, do_cpu):
 
 def main():
     args = parse()
+    ensure_world(args)  # before any GPU call: may start the N ranks and exit
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -356,6 +418,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.plumbing:
+        if world > 1:
+            dist.init_process_group("gloo")
+        return plumbing(args, world, rank)
     if world > 1:
         # nccl = RCCL over xGMI (one rank per GPU).  RT2_BENCH_BACKEND=gloo is a
         # rehearsal mode for boxes with fewer GPUs than ranks (ranks share

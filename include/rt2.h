@@ -233,7 +233,12 @@ int rt2_comm_check(rt2_comm* comm);
  * 16-byte pixels (an rgba32f image or the uint32x4 8-bit sums), device memory —
  * to `root` with one ncclGather and un-interleaves it there into d_image
  * (height*width pixels, device; ignored on other ranks).  shard.rank/nranks
- * must be the communicator's.  Asynchronous on `stream`. */
+ * must be the communicator's.  Asynchronous on `stream`.  Every rank issues the
+ * one ncclGather even when it fails locally (a root without d_image gathers
+ * into scratch, then returns < 0); a local failure that cannot take part (out
+ * of device memory, a shard that does not match the communicator) aborts an
+ * owned communicator (ncclCommAbort: the peers' gather fails instead of
+ * blocking; destroy it afterwards) — a wrapped one is left to its owner. */
 int rt2_gather_slabs(rt2_comm* comm, const void* d_slab, int32_t width, int32_t height, rt2_shard shard,
                      int32_t root, void* d_image, void* stream);
 /* The root's un-interleave alone: d_gathered = [nranks][max_rows][width]
@@ -245,7 +250,12 @@ int rt2_unshard_slabs(const void* d_gathered, int32_t max_rows, int32_t width, i
  * slabs (and, if out_rgb8, the 8-bit sums) are gathered to `root`, which
  * receives the whole image in out_rgba (height*width*4 floats) / out_rgb8
  * (height*width*3 bytes, not flipped); other ranks' output pointers are
- * ignored.  Blocking; every rank must call it. */
+ * ignored.  Blocking; every rank must call it.  The 8-bit sums are accumulated
+ * and gathered when ANY rank passes out_rgb8 (so ranks may pass different
+ * pointers), and the ranks agree before the gather that every one of them
+ * rendered (two 2-int ncclAllReduce(max) steps): a rank-local failure makes
+ * every rank return < 0 ("a peer rank failed") instead of leaving peers
+ * blocked in the gather. */
 int rt2_render_host_gather(rt2_scene* scene, const rt2_uniforms* uniforms, uint32_t frame_begin,
                            uint32_t frame_count, rt2_shard shard, rt2_comm* comm, int32_t root,
                            float* out_rgba, uint8_t* out_rgb8);

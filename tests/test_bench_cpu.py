@@ -102,3 +102,30 @@ def test_kernel_labels():
     assert bench.kernel_label("bvh3/256/t16/w5").startswith("render_bvh3")
     assert bench.kernel_label("smem/256/max3f8/coop32/w6/lockstep").startswith("render_smem")
     assert bench.kernel_label(None) is None
+
+
+def _run_bench(args, env_extra=None, timeout=240):
+    import subprocess
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, cwd=ROOT,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def test_bench_gpus_flag_starts_its_own_ranks():
+    """`bench.py --gpus 2` without a launcher starts 2 ranks itself (gloo here,
+    --plumbing: the launch + row-tile gather path with no GPU) and reports
+    n_gpus 2 with the gathered image checked on rank 0."""
+    r = _run_bench(["--gpus", "2", "--no-cpu-baseline", "--plumbing", "--tile-rows", "3"],
+                   {"RT2_BENCH_BACKEND": "gloo"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    assert lines[0]["n_gpus"] == 2 and lines[0]["gather_ok"] is True
+    assert lines[0]["config"]["parallelism"] == "row-tile x2"
+
+
+def test_bench_gpus_must_match_launcher_world():
+    r = _run_bench(["--gpus", "4", "--plumbing"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
