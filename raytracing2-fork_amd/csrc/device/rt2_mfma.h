@@ -53,11 +53,20 @@ struct MfmaSpec {
     bool ymma = false;      // Y = tn - bk det by a matrix product too (-tn record x ray fragment (-w, -1)): no FMA per pair
     int tshift = 10;        // T = 2^-tshift (Omax + A + 1); 12 for the ymma product variants
     int lds_pad = 0;        // extra static LDS per workgroup (bytes): caps the resident workgroups (experiments)
+    bool k16 = false;       // sweep_k16: v_mfma_f32_32x32x16_f16 on 32-triangle groups, 8 products per 32 rays
+    bool afrag_lds = false; // k16: the ray fragments are re-read from LDS every group (fewer VGPRs)
+    bool rsplit = false;    // k16: scheduling fence between the two 32-ray blocks (one block's terms live at a time)
+    int sol = 0;            // speed-of-light probes (WRONG images; diag clocks only): 1 = every group reads group
+                            // 0's records, 2 = no exact phase, 3 = 2 + only the U term is reduced
 };
 
 // per-wave diagnostic counts of sweep_mfma (wave-uniform; MfmaSpec::diag)
 struct MfmaDiag {
     unsigned long long groups = 0, hot = 0, exact = 0;
+    // shader clocks (s_memtime) of the loop's phases, per wave: item refill +
+    // ray generation (advance), the closest-hit sweep, shading, the
+    // cooperative drain
+    unsigned long long t_advance = 0, t_sweep = 0, t_shade = 0, t_tail = 0;
 };
 
 // per wave: the ray fragments' staging rows (80-B stride: conflict-free
@@ -67,97 +76,116 @@ struct MfmaWaveLds {
     float bk[64];
 };
 
-// Triangle records (one thread per padded triangle), in binary64 from the
-// pre-transformed f32 triangle.  A triangle outside the validated range (as
-// sweep_plk's: |a_i| <= 2^20, e0/e1/n components 0 or in [2^-100, 2^20],
-// max >= 2^-30; non-finite) gets all-zero coefficients, which always pass
-// (the exact test decides); padding triangles get -tn = +2^13, which never
-// passes.  flags[0] += out-of-range triangles, flags[1] = max |a_i| (float bits).
+// Filter coefficients of padded triangle i (binary64, from the pre-transformed
+// f32 triangle) and its record scale tau (a power of two that puts the largest
+// coefficient in [2^13, 2^14)).  A triangle outside the validated range (as
+// sweep_plk's: |a_i| <= 2^20, e0/e1/n components 0 or in [2^-100, 2^20], max
+// >= 2^-30; non-finite) gets all-zero coefficients, which always pass (the
+// exact test decides); padding triangles get -tn = +2^13, which never passes.
+// flags[0] += out-of-range triangles, flags[1] = max |a_i| (float bits).
+// Shared by both record layouts (prep_mfma, prep_mfma_k16).
+struct MfmaCoef {
+    double c[kMfmaQ][10];  // quantity x ray slot (d.xyz, m.xyz, o.xyz, 1)
+    double tau;
+};
+__device__ __forceinline__ void mfma_coefs(const float4* tri, int i, int n, MfmaCoef& k, uint32_t* flags) {
+    for (int q = 0; q < kMfmaQ; q++)
+        for (int c = 0; c < 10; c++) k.c[q][c] = 0.0;
+    k.tau = 1.0;
+    if (i >= n) {
+        k.c[3][9] = 0x1p13;  // padding: -tn' = 2^13 sigma > T
+        return;
+    }
+    const float4 t0 = tri[3 * i], t1 = tri[3 * i + 1], t2 = tri[3 * i + 2];
+    const float a[3] = {t0.x, t0.y, t0.z}, e0[3] = {t0.w, t1.x, t1.y}, e1[3] = {t1.z, t1.w, t2.x},
+                nn[3] = {t2.y, t2.z, t2.w};
+    bool ok = true;
+    float A = 0.0f, M = 0.0f;
+    for (int j = 0; j < 3; j++) {
+        ok = ok && fabsf(a[j]) <= 0x1p20f;
+        A = fmaxf(A, fabsf(a[j]));
+        for (float x : {e0[j], e1[j], nn[j]}) {
+            const float ax = fabsf(x);
+            ok = ok && (x == 0.0f || (ax >= 0x1p-100f && ax <= 0x1p20f));
+            M = fmaxf(M, ax);
+        }
+    }
+    ok = ok && M >= 0x1p-30f;
+    if (!ok) {
+        atomicAdd(&flags[0], 1u);
+        return;
+    }
+    int ex;
+    (void)frexpf(M, &ex);
+    const double s = ldexp(1.0, 1 - ex);
+    double E0[3], E1[3], N[3], P0[3], P1[3], A0[3];
+    for (int j = 0; j < 3; j++) {
+        E0[j] = s * e0[j];
+        E1[j] = s * e1[j];
+        N[j] = s * nn[j];
+        A0[j] = a[j];
+    }
+    P0[0] = A0[1] * E0[2] - A0[2] * E0[1];
+    P0[1] = A0[2] * E0[0] - A0[0] * E0[2];
+    P0[2] = A0[0] * E0[1] - A0[1] * E0[0];
+    P1[0] = A0[1] * E1[2] - A0[2] * E1[1];
+    P1[1] = A0[2] * E1[0] - A0[0] * E1[2];
+    P1[2] = A0[0] * E1[1] - A0[1] * E1[0];
+    const double AN = A0[0] * N[0] + A0[1] * N[1] + A0[2] * N[2];
+    for (int j = 0; j < 3; j++) {
+        k.c[0][j] = -P1[j];                                // U: d
+        k.c[0][3 + j] = E1[j];                             //    m
+        k.c[1][j] = P0[j];                                 // -V: d
+        k.c[1][3 + j] = -E0[j];                            //     m
+        k.c[2][j] = P1[j] - P0[j] + (double)kMfmaC * N[j];  // X: d
+        k.c[2][3 + j] = E0[j] - E1[j];                     //    m
+        k.c[3][6 + j] = -N[j];                             // -tn: o
+        k.c[4][j] = N[j];                                  // dn: d
+    }
+    k.c[3][9] = AN;  // -tn: 1
+    double mx = 0.0;
+    for (int q = 0; q < kMfmaQ; q++)
+        for (int c = 0; c < 10; c++) mx = fmax(mx, fabs(k.c[q][c]));
+    int e2;
+    (void)frexp(mx, &e2);  // mx in [2^(e2-1), 2^e2)
+    k.tau = ldexp(1.0, 14 - e2);
+    atomicMax(&flags[1], __float_as_uint(A));
+}
+
+// The 32 k-slots of one quantity's record: coefficient c < 9 as (hi, hi, lo)
+// against the ray's (hi, lo, hi) in slots 3c..3c+2 (hi*hi + hi*lo + lo*hi),
+// the constant as (hi, lo) against (sigma, sigma) in slots 27, 28.
+__device__ __forceinline__ void mfma_slots(const double* coef, double tau, _Float16 slot[32]) {
+    for (int k = 0; k < 32; k++) slot[k] = (_Float16)0.0f;
+    for (int c = 0; c < 10; c++) {
+        const double v = coef[c] * tau;
+        const _Float16 hi = (_Float16)(float)v;
+        const _Float16 lo = (_Float16)(float)(v - (double)(float)hi);
+        if (c < 9) {
+            slot[3 * c] = hi;      // x hi * ray hi
+            slot[3 * c + 1] = hi;  // x hi * ray lo
+            slot[3 * c + 2] = lo;  // x lo * ray hi
+        } else {
+            slot[27] = hi;  // * sigma
+            slot[28] = lo;  // * sigma
+        }
+    }
+}
+
+// Records in the v_mfma_f32_16x16x32_f16 B-operand order (one thread per
+// padded triangle): [16-group][quantity][lane][8 f16] (5 KiB per 16 triangles).
 __global__ void prep_mfma(const float4* tri, int n, int n_pad, _Float16* out, float* tau_out, uint32_t* flags) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_pad) return;
-    double coef[kMfmaQ][10];
-    for (int q = 0; q < kMfmaQ; q++)
-        for (int c = 0; c < 10; c++) coef[q][c] = 0.0;
-    double tau = 1.0;
-    if (i >= n) {
-        coef[3][9] = 0x1p13;  // padding: -tn' = 2^13 sigma > T
-    } else {
-        const float4 t0 = tri[3 * i], t1 = tri[3 * i + 1], t2 = tri[3 * i + 2];
-        const float a[3] = {t0.x, t0.y, t0.z}, e0[3] = {t0.w, t1.x, t1.y}, e1[3] = {t1.z, t1.w, t2.x},
-                    nn[3] = {t2.y, t2.z, t2.w};
-        bool ok = true;
-        float A = 0.0f, M = 0.0f;
-        for (int k = 0; k < 3; k++) {
-            ok = ok && fabsf(a[k]) <= 0x1p20f;
-            A = fmaxf(A, fabsf(a[k]));
-            for (float x : {e0[k], e1[k], nn[k]}) {
-                const float ax = fabsf(x);
-                ok = ok && (x == 0.0f || (ax >= 0x1p-100f && ax <= 0x1p20f));
-                M = fmaxf(M, ax);
-            }
-        }
-        ok = ok && M >= 0x1p-30f;
-        if (ok) {
-            int ex;
-            (void)frexpf(M, &ex);
-            const double s = ldexp(1.0, 1 - ex);
-            double E0[3], E1[3], N[3], P0[3], P1[3], A0[3];
-            for (int k = 0; k < 3; k++) {
-                E0[k] = s * e0[k];
-                E1[k] = s * e1[k];
-                N[k] = s * nn[k];
-                A0[k] = a[k];
-            }
-            P0[0] = A0[1] * E0[2] - A0[2] * E0[1];
-            P0[1] = A0[2] * E0[0] - A0[0] * E0[2];
-            P0[2] = A0[0] * E0[1] - A0[1] * E0[0];
-            P1[0] = A0[1] * E1[2] - A0[2] * E1[1];
-            P1[1] = A0[2] * E1[0] - A0[0] * E1[2];
-            P1[2] = A0[0] * E1[1] - A0[1] * E1[0];
-            const double AN = A0[0] * N[0] + A0[1] * N[1] + A0[2] * N[2];
-            for (int k = 0; k < 3; k++) {
-                coef[0][k] = -P1[k];                               // U: d
-                coef[0][3 + k] = E1[k];                            //    m
-                coef[1][k] = P0[k];                                // -V: d
-                coef[1][3 + k] = -E0[k];                           //     m
-                coef[2][k] = P1[k] - P0[k] + (double)kMfmaC * N[k];  // X: d
-                coef[2][3 + k] = E0[k] - E1[k];                    //    m
-                coef[3][6 + k] = -N[k];                            // -tn: o
-                coef[4][k] = N[k];                                 // dn: d
-            }
-            coef[3][9] = AN;  // -tn: 1
-            double mx = 0.0;
-            for (int q = 0; q < kMfmaQ; q++)
-                for (int c = 0; c < 10; c++) mx = fmax(mx, fabs(coef[q][c]));
-            int e2;
-            (void)frexp(mx, &e2);  // mx in [2^(e2-1), 2^e2)
-            tau = ldexp(1.0, 14 - e2);
-            atomicMax(&flags[1], __float_as_uint(A));
-        } else {
-            atomicAdd(&flags[0], 1u);
-        }
-    }
+    MfmaCoef k;
+    mfma_coefs(tri, i, n, k, flags);
     const int G = i >> 4, t = i & 15;
     for (int q = 0; q < kMfmaQ; q++) {
         _Float16 slot[32];
-        for (int k = 0; k < 32; k++) slot[k] = (_Float16)0.0f;
-        for (int c = 0; c < 10; c++) {
-            const double v = coef[q][c] * tau;
-            const _Float16 hi = (_Float16)(float)v;
-            const _Float16 lo = (_Float16)(float)(v - (double)(float)hi);
-            if (c < 9) {
-                slot[3 * c] = hi;  // x hi * ray hi
-                slot[3 * c + 1] = hi;  // x hi * ray lo
-                slot[3 * c + 2] = lo;  // x lo * ray hi
-            } else {
-                slot[27] = hi;  // * sigma
-                slot[28] = lo;  // * sigma
-            }
-        }
-        for (int k = 0; k < 32; k++) out[((size_t)(G * kMfmaQ + q) * 64 + 16 * (k >> 3) + t) * 8 + (k & 7)] = slot[k];
+        mfma_slots(k.c[q], k.tau, slot);
+        for (int s = 0; s < 32; s++) out[((size_t)(G * kMfmaQ + q) * 64 + 16 * (s >> 3) + t) * 8 + (s & 7)] = slot[s];
     }
-    tau_out[i] = (float)tau;
+    tau_out[i] = (float)k.tau;
 }
 
 __device__ __forceinline__ float wave_max(float x) {
@@ -166,6 +194,80 @@ __device__ __forceinline__ float wave_max(float x) {
 }
 
 __device__ __forceinline__ float abs_max3(const f3& v) { return fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fabsf(v.z)); }
+
+// Per-wave, per-segment scales of the matrix filter (shared by every sweep
+// layout and by the filter probe): sigma puts the rays' largest |o|, |m| (and,
+// ymma, |o + bk d| for every usable bound) in [2^13, 2^14); Tw = sigma * T
+// with T = 2^-tshift (Omax + A + 1); Bmax = the largest usable distance bound.
+// False (wave-uniform) when a ray is outside the filter's range: the caller
+// sweeps with the scalar-path filter.
+struct MfmaScale {
+    float sigma, Tw, Bmax;
+};
+template <MfmaSpec S>
+__device__ __forceinline__ bool mfma_scale(float mfma_A, const f3& o, const f3& d, const f3& m, MfmaScale& sc) {
+    if (__ballot(!(abs_max3(o) <= 0x1p20f && abs_max3(d) <= 1.0001f))) return false;  // NaN fails too
+    const float Omax = wave_max(abs_max3(o));
+    const float R0 = Omax + mfma_A + 1.0f;
+    float mx = fmaxf(fmaxf(Omax, wave_max(abs_max3(m))), 1.0f);
+    if constexpr (S.ymma) mx = fmaxf(mx, __builtin_fmaf(2.25f, R0, Omax));  // |o + bk d| for every bk <= Bmax
+    int ex;
+    (void)frexpf(mx, &ex);
+    sc.sigma = ldexpf(1.0f, 14 - ex);  // sigma * mx in [2^13, 2^14)
+    sc.Tw = sc.sigma * (ldexpf(kMfmaTs, 10 - S.tshift) * R0);
+    sc.Bmax = kMfmaB * R0;
+    return true;
+}
+
+// This lane's ray vector (sigma-scaled d, m, o, 1) as the 32 f16 k-slots
+// (hi, lo, hi per component against the records' hi, hi, lo), stored as four
+// 16-byte pieces at `row`.
+__device__ __forceinline__ void mfma_main_row(_Float16* row, const f3& d, const f3& m, const f3& o, float sigma) {
+    const float comp[9] = {d.x, d.y, d.z, m.x, m.y, m.z, o.x, o.y, o.z};
+    _Float16 s[32];
+#pragma unroll
+    for (int c = 0; c < 9; c++) {
+        const float v = comp[c] * sigma;
+        const _Float16 hi = (_Float16)v;
+        const _Float16 lo = (_Float16)(v - (float)hi);
+        s[3 * c] = hi;
+        s[3 * c + 1] = lo;
+        s[3 * c + 2] = hi;
+    }
+    s[27] = s[28] = (_Float16)sigma;
+    s[29] = s[30] = s[31] = (_Float16)0.0f;
+    h8* r = reinterpret_cast<h8*>(row);
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        r[k] = h8{s[8 * k], s[8 * k + 1], s[8 * k + 2], s[8 * k + 3], s[8 * k + 4], s[8 * k + 5], s[8 * k + 6],
+                  s[8 * k + 7]};
+}
+
+// The Y fragment's k-slots 16..31 for this lane's distance bound bkv: w = o +
+// bkv d (bkv <= Bmax) with the constant slot -sigma, so that the -tn record
+// gives Y = w.N - AN = s (tnum - bkv det); or, with no usable bound, w = Bmax d
+// and constant 0: Y = -s Bmax det (the det > 0 test).  -w sigma as f16 hi/lo
+// in the o slots (18..26, hi lo hi like the main fragment); slots 0..15 are 0.
+__device__ __forceinline__ void mfma_y_chunk(_Float16 s[16], const f3& d, const f3& o, float bkv, float sigma,
+                                             float Bmax) {
+    const bool fin = bkv <= Bmax;
+    const float wx = fin ? __builtin_fmaf(bkv, d.x, o.x) : Bmax * d.x;
+    const float wy = fin ? __builtin_fmaf(bkv, d.y, o.y) : Bmax * d.y;
+    const float wz = fin ? __builtin_fmaf(bkv, d.z, o.z) : Bmax * d.z;
+    const float wc[3] = {wx, wy, wz};
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        const float v = -wc[c] * sigma;
+        const _Float16 hi = (_Float16)v;
+        const _Float16 lo = (_Float16)(v - (float)hi);
+        s[2 + 3 * c] = hi;
+        s[3 + 3 * c] = lo;
+        s[4 + 3 * c] = hi;
+    }
+    s[0] = s[1] = (_Float16)0.0f;  // slots 16, 17: m.z (zero here)
+    s[11] = s[12] = (_Float16)(fin ? -sigma : 0.0f);
+    s[13] = s[14] = s[15] = (_Float16)0.0f;
+}
 
 // Closest hit of every lane's ray (o, d) over the 16-triangle groups [G0, G1)
 // (all of them by default); the whole wave calls it (lanes without a ray of
@@ -176,38 +278,13 @@ __device__ __forceinline__ bool sweep_mfma(const RenderParams& p, MfmaWaveLds& s
                                            int& bi, float& bestK, MfmaDiag& dg, int G0 = 0, int G1 = -1) {
     const int lane = (int)lane_id();
     const f3 m = cross(d, o);
-    if (__ballot(!(abs_max3(o) <= 0x1p20f && abs_max3(d) <= 1.0001f))) return false;  // NaN fails too
-    const float Omax = wave_max(abs_max3(o));
-    const float R0 = Omax + p.mfma_A + 1.0f;
-    float mx = fmaxf(fmaxf(Omax, wave_max(abs_max3(m))), 1.0f);
-    if constexpr (S.ymma) mx = fmaxf(mx, __builtin_fmaf(2.25f, R0, Omax));  // |o + bk d| for every bk <= Bmax
-    int ex;
-    (void)frexpf(mx, &ex);
-    const float sigma = ldexpf(1.0f, 14 - ex);  // sigma * mx in [2^13, 2^14)
-    const float Tw = sigma * (ldexpf(kMfmaTs, 10 - S.tshift) * R0);
+    MfmaScale sc;
+    if (!mfma_scale<S>(p.mfma_A, o, d, m, sc)) return false;
+    const float sigma = sc.sigma, Tw = sc.Tw, Bmax = sc.Bmax;
     const float Cw = -kMfmaE * sigma;
-    const float Bmax = kMfmaB * R0;
 
     // this lane's ray vector (sigma-scaled d, m, o, 1) as f16 slots -> LDS row `lane`
-    {
-        const float comp[9] = {d.x, d.y, d.z, m.x, m.y, m.z, o.x, o.y, o.z};
-        _Float16 s[32];
-#pragma unroll
-        for (int c = 0; c < 9; c++) {
-            const float v = comp[c] * sigma;
-            const _Float16 hi = (_Float16)v;
-            const _Float16 lo = (_Float16)(v - (float)hi);
-            s[3 * c] = hi;
-            s[3 * c + 1] = lo;
-            s[3 * c + 2] = hi;
-        }
-        s[27] = s[28] = (_Float16)sigma;
-        s[29] = s[30] = s[31] = (_Float16)0.0f;
-        h8* row = reinterpret_cast<h8*>(&sh.ray[lane][0]);
-#pragma unroll
-        for (int k = 0; k < 4; k++) row[k] = h8{s[8 * k], s[8 * k + 1], s[8 * k + 2], s[8 * k + 3], s[8 * k + 4],
-                                                s[8 * k + 5], s[8 * k + 6], s[8 * k + 7]};
-    }
+    mfma_main_row(&sh.ray[lane][0], d, m, o, sigma);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -216,30 +293,11 @@ __device__ __forceinline__ bool sweep_mfma(const RenderParams& p, MfmaWaveLds& s
     for (int R = 0; R < 4; R++) ra[R] = *reinterpret_cast<const h8*>(&sh.ray[16 * R + (lane & 15)][8 * (lane >> 4)]);
     f4v bk[4];
     h8 ya[4];  // ymma: the Y fragment (-w, -1) / (-Bmax d, 0), built in the same LDS rows
-    // Y fragment of this lane's ray for its distance bound bkv: w = o + bkv d
-    // (bkv <= Bmax) with the constant slot -sigma, so that the -tn record gives
-    // Y = w.N - AN = s (tnum - bkv det); or, with no usable bound, w = Bmax d
-    // and constant 0: Y = -s Bmax det (the det > 0 test).  -w sigma as f16
-    // hi/lo in the o slots (18..26, hi lo hi like the main fragment).
+    // Y fragment of this lane's ray for its distance bound bkv (mfma_y_chunk),
+    // built in the same LDS rows (slots 0..15 zero)
     auto build_y = [&](float bkv) {
-        const bool fin = bkv <= Bmax;
-        const float wx = fin ? __builtin_fmaf(bkv, d.x, o.x) : Bmax * d.x;
-        const float wy = fin ? __builtin_fmaf(bkv, d.y, o.y) : Bmax * d.y;
-        const float wz = fin ? __builtin_fmaf(bkv, d.z, o.z) : Bmax * d.z;
-        const float wc[3] = {wx, wy, wz};
         _Float16 s[16];
-#pragma unroll
-        for (int c = 0; c < 3; c++) {
-            const float v = -wc[c] * sigma;
-            const _Float16 hi = (_Float16)v;
-            const _Float16 lo = (_Float16)(v - (float)hi);
-            s[2 + 3 * c] = hi;
-            s[3 + 3 * c] = lo;
-            s[4 + 3 * c] = hi;
-        }
-        s[0] = s[1] = (_Float16)0.0f;  // slots 16, 17: d.z (zero here)
-        s[11] = s[12] = (_Float16)(fin ? -sigma : 0.0f);
-        s[13] = s[14] = s[15] = (_Float16)0.0f;
+        mfma_y_chunk(s, d, o, bkv, sigma, Bmax);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();  // every lane has read the rows' previous contents
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -354,13 +412,299 @@ __device__ __forceinline__ bool sweep_mfma(const RenderParams& p, MfmaWaveLds& s
     return true;
 }
 
+
+// ---------------------------------------------------------------------------
+// The k16 sweep (MfmaSpec::k16): the same filter on v_mfma_f32_32x32x16_f16.
+// A 32x32 product with K = 16 yields 1,024 terms per 32 matrix cycles, twice
+// the terms per cycle of the 16x16x32 form whenever a quantity fits 16 k-slots.
+// The ray vector's 32 slots are two K-halves: [d (9), m.x m.y m.z-hi (7)] and
+// [m.z lo/hi (2), o (9), constant (2), 0 (3)].  U, -V and X use d and m (18
+// slots): two chained products each; -tn uses o and the constant (second half
+// only) and Y the second half of its own fragment: one product each.  So a
+// 32-ray x 32-triangle block takes 8 MFMAs — 256 matrix cycles and 64 cycles
+// of MFMA issue on the VALU port per 1,024 pairs, against 320 and 160 for 20
+// v_mfma_f32_16x16x32_f16 — and the same 2 v_max3_i32 + 1/2 v_min3 per pair.
+// Operand maps (32x32x16, K = 16): lane l holds A[row l&31][k 8(l>>5)+j] and
+// B[k 8(l>>5)+j][col l&31]; D: column l&31 in all 16 registers (rows
+// 8(i>>2) + 4(l>>5) + (i&3)), so every term a lane holds belongs to triangle
+// 32G + (l&31): min over them, one ballot, lanes l and l+32 share a triangle.
+// Records: [32-group][op][lane][8 f16], ops U0 U1 V0 V1 X0 X1 T1 (7 KiB per 32
+// triangles); tau per triangle.  The arithmetic of every product — the same
+// f16 hi/lo slots, the same scales — is the 16x16x32 form's, so its error
+// budget applies unchanged ("The matrix filter"); the probe
+// (mfma_probe_kernel) measures both forms on the hardware.
+constexpr int kK16Ops = 7;
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+struct MfmaK16Lds {
+    // slots 0..31: the main fragment; 32..47: the Y fragment's slots 16..31
+    // (112-B rows: 16-B reads of 16 consecutive rows hit distinct banks)
+    _Float16 ray[64][56];
+};
+
+__global__ void prep_mfma_k16(const float4* tri, int n, int n_pad, _Float16* out, float* tau_out, uint32_t* flags) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_pad) return;
+    MfmaCoef k;
+    mfma_coefs(tri, i, n, k, flags);
+    const int G = i >> 5, t = i & 31;
+    for (int op = 0; op < kK16Ops; op++) {
+        const int q = op < 6 ? op >> 1 : 3, h = op < 6 ? (op & 1) : 1;
+        _Float16 slot[32];
+        mfma_slots(k.c[q], k.tau, slot);
+        for (int j = 0; j < 16; j++)
+            out[((size_t)(G * kK16Ops + op) * 64 + t + 32 * (j >> 3)) * 8 + (j & 7)] = slot[16 * h + j];
+    }
+    tau_out[i] = (float)k.tau;
+}
+
+// The five terms of 32 rays (fragments a0/a1 = the main fragment's two
+// K-halves, y1 = the Y fragment's second half) x 32 triangles (records b[7]).
+struct K16Terms {
+    f16v U, V, X, T, Y;
+};
+__device__ __forceinline__ K16Terms k16_terms(const h8& a0, const h8& a1, const h8& y1, const h8* b) {
+    const f16v zero = {};
+    K16Terms r;
+    r.U = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b[0], zero, 0, 0, 0);
+    r.V = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b[2], zero, 0, 0, 0);
+    r.X = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b[4], zero, 0, 0, 0);
+    r.U = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b[1], r.U, 0, 0, 0);
+    r.V = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b[3], r.V, 0, 0, 0);
+    r.X = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b[5], r.X, 0, 0, 0);
+    r.T = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b[6], zero, 0, 0, 0);
+    r.Y = __builtin_amdgcn_mfma_f32_32x32x16_f16(y1, b[6], zero, 0, 0, 0);
+    return r;
+}
+
+template <MfmaSpec S>
+__device__ __forceinline__ bool sweep_k16(const RenderParams& p, MfmaK16Lds& sh, const f3& o, const f3& d, float& best,
+                                          int& bi, float& bestK, MfmaDiag& dg) {
+    static_assert(S.ymma && S.imax && S.minred, "the k16 sweep implements the ymma / imax / minred form");
+    const int lane = (int)lane_id();
+    const int r32 = lane & 31, hl = lane >> 5;
+    const f3 m = cross(d, o);
+    MfmaScale sc;
+    if (!mfma_scale<S>(p.mfma_A, o, d, m, sc)) return false;
+    mfma_main_row(&sh.ray[lane][0], d, m, o, sc.sigma);
+    auto write_y = [&](float bkv) {
+        _Float16 s[16];
+        mfma_y_chunk(s, d, o, bkv, sc.sigma, sc.Bmax);
+        h8* row = reinterpret_cast<h8*>(&sh.ray[lane][32]);
+        row[0] = h8{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7]};
+        row[1] = h8{s[8], s[9], s[10], s[11], s[12], s[13], s[14], s[15]};
+    };
+    write_y(bestK);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    h8 a0[2], a1[2], y1[2];
+    auto read_a = [&]() {
+#pragma unroll
+        for (int R = 0; R < 2; R++) {
+            a0[R] = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][8 * hl]);
+            a1[R] = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][16 + 8 * hl]);
+        }
+    };
+    auto read_y = [&]() {
+#pragma unroll
+        for (int R = 0; R < 2; R++) y1[R] = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][32 + 8 * hl]);
+    };
+    if constexpr (!S.afrag_lds) read_a();
+    read_y();
+
+    const int ng = (p.n_tris + 31) >> 5;
+    const h8* fg = reinterpret_cast<const h8*>(p.mfma_k16_frag) + lane;
+    const float* tg = p.mfma_k16_tau + r32;
+    h8 b[kK16Ops], nb[kK16Ops];
+    float tau = 0.0f, ntau = 0.0f;
+    auto fetch = [&](h8* dst, float& t) {
+#pragma unroll
+        for (int op = 0; op < kK16Ops; op++) dst[op] = fg[64 * op];
+        t = *tg;
+        fg += kK16Ops * 64;
+        tg += 32;
+    };
+    if constexpr (S.prefetch) fetch(nb, ntau);
+    for (int G = 0; G < ng; G++) {
+        if constexpr (S.prefetch) {
+            // this group's records arrived during the previous group's
+            // products; the next group's are requested before this group's
+#pragma unroll
+            for (int op = 0; op < kK16Ops; op++) b[op] = nb[op];
+            tau = ntau;
+            if (G + 1 < ng) fetch(nb, ntau);
+        } else if constexpr (S.sol == 1) {
+            if (G == 0) fetch(b, tau);
+        } else {
+            fetch(b, tau);
+        }
+        if constexpr (S.afrag_lds) read_a();
+        const float Tl = tau * sc.Tw;
+        int tmin = 0x7fffffff;
+#pragma unroll
+        for (int R = 0; R < 2; R++) {
+            const K16Terms q = k16_terms(a0[R], a1[R], y1[R], b);
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                // max of the five terms on their bit patterns (see sweep_mfma)
+                if constexpr (S.sol == 3) {
+                    tmin = min(tmin, __float_as_int(q.U[i]));
+                } else {
+                    const int t3 = max(max(__float_as_int(q.U[i]), __float_as_int(q.V[i])), __float_as_int(q.X[i]));
+                    const int t = max(max(t3, __float_as_int(q.T[i])), __float_as_int(q.Y[i]));
+                    tmin = min(tmin, t);
+                }
+            }
+            if constexpr (S.rsplit) __builtin_amdgcn_sched_barrier(0);
+        }
+        const unsigned long long M = S.sol >= 2 ? (unsigned long long)(tmin == 0x7ffffffe) : __ballot(tmin <= __float_as_int(Tl));
+        if constexpr (S.diag) dg.groups += 1;
+        if (M) {
+            if constexpr (S.diag) dg.hot += 1;
+            // triangles of the group with a passing pair: the exact phase, in index order
+            uint32_t m32 = (uint32_t)(M | M >> 32);
+            const float bk0 = bestK;
+            while (m32) {
+                const int t = __builtin_ctz(m32);
+                m32 &= m32 - 1;
+                const int idx = 32 * G + t;
+                if (idx >= p.n_tris) break;
+                if constexpr (S.diag) dg.exact += 1;
+                cfloat* tp = (cfloat*)p.tri + 12 * idx;
+                const MtQ qq = mt_quantities(o, d, ldc4(tp), ldc4(tp + 4), ldc4(tp + 8));
+                if (mt_pass3(qq, bestK)) mt_exact(qq, idx, best, bi, bestK);
+            }
+            if (__ballot(bestK != bk0)) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();  // every lane has read the rows' previous Y slots
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                write_y(bestK);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                read_y();
+            }
+        }
+    }
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// Filter probe (test hook rt2_mfma_probe, not part of the render): the five
+// filter terms of every (ray, triangle) pair exactly as a product sweep
+// computes them — the same scales (mfma_scale), fragments (mfma_main_row,
+// mfma_y_chunk, through the same LDS rows), records and MFMA instructions —
+// written out instead of reduced, with the operand fragments and the
+// reference's own accept decision (mt_quantities + mt_exact against the ray's
+// bound), so the host can measure the products' error against a binary64
+// evaluation of the same operands and check the filter's conservativeness on
+// the hardware.  One wave per 64 rays (n_rays a multiple of 64).
+//   rays:   per ray {o.x, o.y, o.z, best} {d.x, d.y, d.z, 0}
+//   terms:  [ray][tri][5] (U, -V, X, -tn, Y; tri < n_pad)
+//   frags:  [ray][48] f16: main slots 0..31, Y slots 16..31
+//   rinfo:  [ray][8]: in range, sigma, Tw, Bmax, m.x, m.y, m.z, bestK
+//   accept: [ray][tri] (tri < n_tris): the reference accepts the pair
+template <MfmaSpec S>
+__global__ __launch_bounds__(64) void mfma_probe_kernel(RenderParams p, const float4* rays, int n_pad, float* terms,
+                                                        _Float16* frags, float* rinfo, uint8_t* accept) {
+    __shared__ MfmaK16Lds sh;
+    const int lane = (int)threadIdx.x;
+    const size_t ray = (size_t)blockIdx.x * 64 + lane;
+    const float4 r0 = rays[2 * ray], r1 = rays[2 * ray + 1];
+    const f3 o = mk(r0.x, r0.y, r0.z), d = mk(r1.x, r1.y, r1.z);
+    const float best = r0.w, bestK = best * 1.0009765625f;
+    for (int t = 0; t < p.n_tris; t++) {
+        cfloat* tp = (cfloat*)p.tri + 12 * t;
+        float b = best, bk = bestK;
+        int bi = -1;
+        mt_exact(mt_quantities(o, d, ldc4(tp), ldc4(tp + 4), ldc4(tp + 8)), t, b, bi, bk);
+        accept[ray * p.n_tris + t] = bi == t;
+    }
+    const f3 m = cross(d, o);
+    MfmaScale sc{0.0f, 0.0f, 0.0f};
+    const bool ok = mfma_scale<S>(p.mfma_A, o, d, m, sc);
+    float* ri = rinfo + ray * 8;
+    ri[0] = ok ? 1.0f : 0.0f;
+    ri[1] = sc.sigma;
+    ri[2] = sc.Tw;
+    ri[3] = sc.Bmax;
+    ri[4] = m.x;
+    ri[5] = m.y;
+    ri[6] = m.z;
+    ri[7] = bestK;
+    if (!ok) return;  // wave-uniform
+    mfma_main_row(&sh.ray[lane][0], d, m, o, sc.sigma);
+    {
+        _Float16 s[16];
+        mfma_y_chunk(s, d, o, bestK, sc.sigma, sc.Bmax);
+        for (int j = 0; j < 16; j++) sh.ray[lane][32 + j] = s[j];
+    }
+    __syncthreads();
+    for (int j = 0; j < 48; j++) frags[ray * 48 + j] = sh.ray[lane][j];
+    const size_t ray0 = (size_t)blockIdx.x * 64;
+    if constexpr (S.k16) {
+        const int r32 = lane & 31, hl = lane >> 5;
+        const h8* fg = reinterpret_cast<const h8*>(p.mfma_k16_frag) + lane;
+        for (int G = 0; G < n_pad / 32; G++) {
+            h8 b[kK16Ops];
+            for (int op = 0; op < kK16Ops; op++) b[op] = fg[(size_t)G * kK16Ops * 64 + 64 * op];
+            for (int R = 0; R < 2; R++) {
+                const h8 a0 = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][8 * hl]);
+                const h8 a1 = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][16 + 8 * hl]);
+                const h8 y1 = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][32 + 8 * hl]);
+                const K16Terms q = k16_terms(a0, a1, y1, b);
+                for (int i = 0; i < 16; i++) {
+                    const size_t rr = ray0 + 32 * R + 8 * (i >> 2) + 4 * hl + (i & 3);
+                    float* tt = terms + (rr * n_pad + 32 * G + r32) * 5;
+                    tt[0] = q.U[i];
+                    tt[1] = q.V[i];
+                    tt[2] = q.X[i];
+                    tt[3] = q.T[i];
+                    tt[4] = q.Y[i];
+                }
+            }
+        }
+    } else {
+        // the 16x16x32 form (sweep_mfma, ymma): A rows in the main/Y LDS rows,
+        // the Y fragment as sweep_mfma builds it (slots 0..15 zero)
+        const h8* fg = reinterpret_cast<const h8*>(p.mfma_frag) + lane;
+        const f4v zero = {0.0f, 0.0f, 0.0f, 0.0f};
+        for (int G = 0; G < n_pad / 16; G++) {
+            const h8 c0 = fg[(size_t)G * kMfmaQ * 64], c1 = fg[(size_t)G * kMfmaQ * 64 + 64],
+                     c2 = fg[(size_t)G * kMfmaQ * 64 + 128], c3 = fg[(size_t)G * kMfmaQ * 64 + 192];
+            for (int R = 0; R < 4; R++) {
+                const int row = 16 * R + (lane & 15), k0 = 8 * (lane >> 4);
+                const h8 ra = *reinterpret_cast<const h8*>(&sh.ray[row][k0]);
+                h8 ya = h8{};
+                if (k0 >= 16) ya = *reinterpret_cast<const h8*>(&sh.ray[row][32 + k0 - 16]);
+                const f4v qU = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra, c0, zero, 0, 0, 0);
+                const f4v qV = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra, c1, zero, 0, 0, 0);
+                const f4v qX = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra, c2, zero, 0, 0, 0);
+                const f4v qT = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra, c3, zero, 0, 0, 0);
+                const f4v qY = __builtin_amdgcn_mfma_f32_16x16x32_f16(ya, c3, zero, 0, 0, 0);
+                for (int i = 0; i < 4; i++) {
+                    const size_t rr = ray0 + 16 * R + 4 * (lane >> 4) + i;
+                    float* tt = terms + (rr * n_pad + 16 * G + (lane & 15)) * 5;
+                    tt[0] = qU[i];
+                    tt[1] = qV[i];
+                    tt[2] = qX[i];
+                    tt[3] = qT[i];
+                    tt[4] = qY[i];
+                }
+            }
+        }
+    }
+}
+
 // MFMA: render_smem's lockstep segment loop and cooperative drain with the
 // matrix-core filter (sweep_mfma) as the closest-hit sweep; a wave whose
 // rays leave the filter's range sweeps with the scalar-path filter instead.
 template <MfmaSpec S>
 __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves))) void render_mfma(RenderParams p) {
-    __shared__ MfmaWaveLds wl[S.block / 64];
-    MfmaWaveLds& sh = wl[threadIdx.x >> 6];
+    using WL = std::conditional_t<S.k16, MfmaK16Lds, MfmaWaveLds>;
+    __shared__ WL wl[S.block / 64];
+    WL& sh = wl[threadIdx.x >> 6];
     if constexpr (S.lds_pad > 0) {
         __shared__ uint32_t pad[S.lds_pad / 4];
         if (p.n_items == 0) pad[threadIdx.x] = 0;  // never taken at launch; keeps the allocation
@@ -368,9 +712,19 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
     Lane L;
     lane_init(L);
     MfmaDiag dg;
+    unsigned long long tc = 0;  // diag: s_memtime at the current phase's start
+    if constexpr (S.diag) tc = __builtin_amdgcn_s_memtime();
+    auto stamp = [&](unsigned long long& acc) {
+        if constexpr (S.diag) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            acc += t - tc;
+            tc = t;
+        }
+    };
     for (;;) {
         advance(L, p);
         const unsigned long long act = __ballot(L.st == ST_TRACE);
+        stamp(dg.t_advance);
         if constexpr (S.lockstep) {
             if (!__syncthreads_or(act != 0)) break;
             if (!act) continue;
@@ -399,6 +753,7 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
                 L.segs += 1;
                 shade(L, p, mybest, mybi);
             }
+            stamp(dg.t_tail);
             continue;
         }
         // lanes without a ray carry the first live lane's (their passes add no triangle)
@@ -409,20 +764,31 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
         const f3 ro = mine ? L.o : o, rd = mine ? L.d : dd;
         float best = 1e38f, bestK = 1e38f * 1.0009765625f;
         int bi = -1;
-        if (!sweep_mfma<S>(p, sh, ro, rd, best, bi, bestK, dg) && mine)
+        bool swept;
+        if constexpr (S.k16)
+            swept = sweep_k16<S>(p, sh, ro, rd, best, bi, bestK, dg);
+        else
+            swept = sweep_mfma<S>(p, sh, ro, rd, best, bi, bestK, dg);
+        if (!swept && mine)
             sweep_masked<8, true, Filter::Max3>(ro, rd, nullptr, (const float*)p.tri, p.n_tris, 0, best, bi, bestK);
+        stamp(dg.t_sweep);
         if (mine) {
             L.bounce += 1;
             L.segs += 1;
             shade(L, p, best, bi);
         }
+        stamp(dg.t_shade);
     }
     flush_counters(L, p);
     if constexpr (S.diag)
         if (lane_id() == 0) {
-            atomicAdd(p.seg_counter + 1, dg.groups);  // (wave, 16-triangle group) sweeps
+            atomicAdd(p.seg_counter + 1, dg.groups);  // (wave, triangle group) sweeps
             atomicAdd(p.seg_counter + 2, dg.hot);     // ... with a passing pair
             atomicAdd(p.seg_counter + 3, dg.exact);   // (wave, triangle) exact tests
+            atomicAdd(p.seg_counter + 8, dg.t_advance);
+            atomicAdd(p.seg_counter + 9, dg.t_sweep);
+            atomicAdd(p.seg_counter + 10, dg.t_shade);
+            atomicAdd(p.seg_counter + 11, dg.t_tail);
         }
 }
 

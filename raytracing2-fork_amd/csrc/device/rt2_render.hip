@@ -25,6 +25,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../../include/rt2.h"
@@ -75,6 +76,8 @@ struct rt2_scene {
     float plk_A = 0.0f;                         // max |a_i| over the triangles
     _Float16* d_mfma = nullptr;                 // render_mfma filter records (rt2_mfma.h)
     float* d_mfma_tau = nullptr;                // per-triangle record scale
+    _Float16* d_mfma_k16 = nullptr;             // sweep_k16 records (32-triangle groups, 7 KiB each)
+    float* d_mfma_k16_tau = nullptr;            // per-triangle record scale (same values as d_mfma_tau)
     int mfma_ok = 0;                            // render_mfma usable (records built, scene in range)
     float mfma_A = 0.0f;                        // max |a_i| over the in-range triangles
     float4* d_fb = nullptr;                     // frame_split scratch (per-frame colours)
@@ -421,6 +424,14 @@ static int scene_init(rt2_scene* s, const rt2_triangle* tris, int32_t n_tris, co
         HIPCHECK(hipMemset(d_mflags, 0, 2 * sizeof(uint32_t)));
         std::memcpy(&s->mfma_A, &mflags[1], sizeof(float));
         s->mfma_ok = s->mfma_A <= 0x1p20f;
+        // the same coefficients in the k16 layout (sweep_k16): 7 KiB per 32 triangles
+        const int n_pad32 = (n_tris + 31) / 32 * 32;
+        HIPCHECK(hipMalloc(&s->d_mfma_k16, (size_t)n_pad32 * kK16Ops * 16 * sizeof(_Float16)));
+        HIPCHECK(hipMalloc(&s->d_mfma_k16_tau, (size_t)n_pad32 * sizeof(float)));
+        hipLaunchKernelGGL(prep_mfma_k16, dim3((n_pad32 + 255) / 256), dim3(256), 0, 0, s->d_tri, n_tris, n_pad32,
+                           s->d_mfma_k16, s->d_mfma_k16_tau, d_mflags);
+        HIPCHECK(hipGetLastError());
+        HIPCHECK(hipMemset(d_mflags, 0, 2 * sizeof(uint32_t)));
     }
     HIPCHECK(hipDeviceSynchronize());
     return 0;
@@ -438,6 +449,8 @@ extern "C" void rt2_scene_destroy(rt2_scene* s) {
     (void)hipFree(s->d_plk);
     (void)hipFree(s->d_mfma);
     (void)hipFree(s->d_mfma_tau);
+    (void)hipFree(s->d_mfma_k16);
+    (void)hipFree(s->d_mfma_k16_tau);
     (void)hipFree(s->d_fb);
     (void)hipFree(s->d_cost);
     (void)hipFree(s->d_order);
@@ -521,6 +534,15 @@ constexpr MfmaSpec kMfmaT8Y{.block = 256, .waves = 2, .tail_lanes = 8, .imax = t
                             .tshift = 12};
 constexpr MfmaSpec kMfmaT8Y4{.block = 256, .waves = 4, .tail_lanes = 8, .imax = true, .minred = true, .ymma = true,
                              .tshift = 12};
+// k16 sweep (v_mfma_f32_32x32x16_f16, 8 products per 1,024 pairs)
+constexpr MfmaSpec k16_spec(int waves, bool afrag_lds = false, bool diag = false, bool rsplit = false,
+                           bool prefetch = false) {
+    return MfmaSpec{.block = 256, .waves = waves, .tail_lanes = 8, .imax = true, .prefetch = prefetch,
+                    .minred = true, .diag = diag, .ymma = true, .tshift = 12, .k16 = true, .afrag_lds = afrag_lds,
+                    .rsplit = rsplit};
+}
+constexpr MfmaSpec kMfmaT8Y4D{.block = 256, .waves = 4, .tail_lanes = 8, .imax = true, .minred = true, .diag = true,
+                              .ymma = true, .tshift = 12};
 constexpr Bvh3Spec kBvhDefault{.block = 256, .thresh = 16, .slab = Slab::Markstein, .waves = 5, .diag = false};
 
 #ifdef RT2_EXPERIMENTS
@@ -574,6 +596,24 @@ const Variant kVariants[] = {
     RT2_VARIANT(152, K_MFMA, render_mfma<kMfmaT8Y4>, 256, "mfma/256/f16x3/coop8/w4/imax/minred/ymma/t12"),  // default (<= kMfmaMaxTris)
     RT2_VARIANT(150, K_MFMA, render_mfma<kMfmaT8Y>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma/t12"),  // 1.5-3 items per lane
     RT2_VARIANT(136, K_SMEM, render_smem<kSmemDefault>, 256, "smem/256/max3f8/coop32/w6/lockstep"),  // variant 0 forced (id 0 = automatic)
+    RT2_VARIANT(160, K_MFMA, render_mfma<k16_spec(3)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12"),
+    RT2_VARIANT(161, K_MFMA, render_mfma<k16_spec(4)>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12"),
+    RT2_VARIANT(162, K_MFMA, render_mfma<k16_spec(2)>, 256, "mfma/256/k16/coop8/w2/imax/minred/ymma/t12"),
+    RT2_VARIANT(163, K_MFMA, render_mfma<k16_spec(4, true)>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/alds"),
+    RT2_VARIANT(164, K_MFMA, render_mfma<k16_spec(3, true)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/alds"),
+    RT2_VARIANT(165, K_MFMA, render_mfma<k16_spec(3, false, true)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/diag"),
+    RT2_VARIANT(169, K_MFMA, render_mfma<kMfmaT8Y4D>, 256, "mfma/256/f16x3/coop8/w4/imax/minred/ymma/t12/diag"),  // 152 + diag
+    RT2_VARIANT(170, K_MFMA, render_mfma<k16_spec(2, false, false, false, true)>, 256, "mfma/256/k16/coop8/w2/imax/minred/ymma/t12/pf"),
+    RT2_VARIANT(171, K_MFMA, render_mfma<k16_spec(3, false, false, false, true)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/pf"),
+    RT2_VARIANT(172, K_MFMA, render_mfma<k16_spec(3, true, false, false, true)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/alds/pf"),
+    RT2_VARIANT(173, K_MFMA, render_mfma<k16_spec(2, true, false, false, true)>, 256, "mfma/256/k16/coop8/w2/imax/minred/ymma/t12/alds/pf"),
+    RT2_VARIANT(174, K_MFMA, render_mfma<k16_spec(3, false, true, false, true)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/pf/diag"),
+    RT2_VARIANT(190, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3, false, true); x.sol = 1; return x; }()>, 256, "SOL1/k16/w3/records-of-group-0"),
+    RT2_VARIANT(191, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3, false, true); x.sol = 2; return x; }()>, 256, "SOL2/k16/w3/no-exact-phase"),
+    RT2_VARIANT(192, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3, false, true); x.sol = 3; return x; }()>, 256, "SOL3/k16/w3/U-only"),
+    RT2_VARIANT(166, K_MFMA, render_mfma<k16_spec(3, false, false, true)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/rsplit"),
+    RT2_VARIANT(167, K_MFMA, render_mfma<k16_spec(4, true, false, true)>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/alds/rsplit"),
+    RT2_VARIANT(168, K_MFMA, render_mfma<k16_spec(3, true, false, true)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/alds/rsplit"),
 #ifdef RT2_EXPERIMENTS
     RT2_VARIANT(140, K_MFMA, render_mfma<kMfmaT8>, 256, "mfma/256/f16x3/coop8/w2/imax/minred"),  // Y by one FMA per pair
     RT2_VARIANT(137, K_MFMA, render_mfma<kMfmaIM>, 256, "mfma/256/f16x3/coop16/w2/imax/minred"),  // drain at 16 live rays
@@ -751,6 +791,8 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     p.mfma_frag = s->d_mfma;
     p.mfma_tau = s->d_mfma_tau;
     p.mfma_A = s->mfma_A;
+    p.mfma_k16_frag = s->d_mfma_k16;
+    p.mfma_k16_tau = s->d_mfma_k16_tau;
     p.tri_mtl = s->d_mtl;
     p.raw = s->d_raw;
     p.texels = s->d_texels;
@@ -1162,4 +1204,93 @@ extern "C" int rt2_device_selftest(const float* in, int32_t n, float* out10) {
     (void)hipFree(din);
     (void)hipFree(dout);
     return 0;
+}
+
+// Not in rt2.h (test hook): copies one of the scene's derived device arrays to
+// host memory: 0 = pre-transformed triangles (3 float4 each), 1 = render_mfma
+// records (16x16x32 layout), 2 = their per-triangle tau, 3 = sweep_k16 records,
+// 4 = their tau.  Returns the array's size in bytes (nothing copied when
+// `host` is null or `bytes` is too small), < 0 on error.
+extern "C" long long rt2_scene_export(rt2_scene* s, int what, void* host, unsigned long long bytes) {
+    if (!s) return -1;
+    const size_t n = (size_t)std::max(s->n_tris, 1), n16 = (size_t)(s->n_tris + 15) / 16 * 16,
+                 n32 = (size_t)(s->n_tris + 31) / 32 * 32;
+    const void* src = nullptr;
+    size_t sz = 0;
+    switch (what) {
+    case 0: src = s->d_tri, sz = n * 3 * sizeof(float4); break;
+    case 1: src = s->d_mfma, sz = n16 * kMfmaQ * 32 * sizeof(_Float16); break;
+    case 2: src = s->d_mfma_tau, sz = n16 * sizeof(float); break;
+    case 3: src = s->d_mfma_k16, sz = n32 * kK16Ops * 16 * sizeof(_Float16); break;
+    case 4: src = s->d_mfma_k16_tau, sz = n32 * sizeof(float); break;
+    default: return -1;
+    }
+    if (!src || s->n_tris == 0) return 0;
+    if (host && bytes >= sz) {
+        HIPCHECK(hipSetDevice(s->device));
+        HIPCHECK(hipDeviceSynchronize());
+        HIPCHECK(hipMemcpy(host, src, sz, hipMemcpyDeviceToHost));
+    }
+    return (long long)sz;
+}
+
+// Not in rt2.h (test hook): the matrix filter's terms on the hardware
+// (mfma_probe_kernel) for n_rays rays (a multiple of 64; 8 floats each: o.xyz,
+// best, d.xyz, 0) against every triangle of the scene.  layout 0 = the
+// 16x16x32 form of render_mfma (variants 150/152), 1 = the k16 form
+// (sweep_k16).  Host outputs, sized by the caller: terms [n_rays][n_pad][5]
+// (n_pad = triangles padded to 16 / 32), frags [n_rays][48] f16 bits, rinfo
+// [n_rays][8], accept [n_rays][n_tris].
+extern "C" int rt2_mfma_probe(rt2_scene* s, int layout, const float* rays, int32_t n_rays, float* terms,
+                              uint16_t* frags, float* rinfo, uint8_t* accept) {
+    if (!s || !rays || n_rays <= 0 || n_rays % 64 != 0 || !terms || !frags || !rinfo || !accept ||
+        (layout != 0 && layout != 1) || s->n_tris < 1 || !s->mfma_ok) {
+        rt2h::set_error("rt2_mfma_probe: bad argument (n_rays a positive multiple of 64, a scene in the filter's "
+                        "range)");
+        return -1;
+    }
+    HIPCHECK(hipSetDevice(s->device));
+    const int n_pad = layout == 1 ? (s->n_tris + 31) / 32 * 32 : (s->n_tris + 15) / 16 * 16;
+    const size_t nr = (size_t)n_rays;
+    const size_t b_rays = nr * 8 * sizeof(float), b_terms = nr * n_pad * 5 * sizeof(float),
+                 b_frags = nr * 48 * sizeof(uint16_t), b_info = nr * 8 * sizeof(float), b_acc = nr * s->n_tris;
+    char* d = nullptr;
+    HIPCHECK(hipMalloc(&d, b_rays + b_terms + b_frags + b_info + b_acc + 64));
+    char* p0 = d;
+    float4* d_rays = (float4*)p0;
+    float* d_terms = (float*)(p0 += b_rays);
+    _Float16* d_frags = (_Float16*)(p0 += b_terms);
+    float* d_info = (float*)(p0 += b_frags);
+    uint8_t* d_acc = (uint8_t*)(p0 += b_info);
+    int rc = 0;
+    auto run = [&]() -> int {
+        HIPCHECK(hipMemcpy(d_rays, rays, b_rays, hipMemcpyHostToDevice));
+        HIPCHECK(hipMemset(d_terms, 0, b_terms));
+        RenderParams p;
+        std::memset(&p, 0, sizeof(p));
+        p.tri = s->d_tri;
+        p.n_tris = s->n_tris;
+        p.mfma_frag = s->d_mfma;
+        p.mfma_tau = s->d_mfma_tau;
+        p.mfma_A = s->mfma_A;
+        p.mfma_k16_frag = s->d_mfma_k16;
+        p.mfma_k16_tau = s->d_mfma_k16_tau;
+        constexpr MfmaSpec k16 = k16_spec(3), f16x32 = kMfmaT8Y4;
+        if (layout == 1)
+            hipLaunchKernelGGL(mfma_probe_kernel<k16>, dim3(n_rays / 64), dim3(64), 0, 0, p, d_rays, n_pad, d_terms,
+                               d_frags, d_info, d_acc);
+        else
+            hipLaunchKernelGGL(mfma_probe_kernel<f16x32>, dim3(n_rays / 64), dim3(64), 0, 0, p, d_rays, n_pad,
+                               d_terms, d_frags, d_info, d_acc);
+        HIPCHECK(hipGetLastError());
+        HIPCHECK(hipDeviceSynchronize());
+        HIPCHECK(hipMemcpy(terms, d_terms, b_terms, hipMemcpyDeviceToHost));
+        HIPCHECK(hipMemcpy(frags, d_frags, b_frags, hipMemcpyDeviceToHost));
+        HIPCHECK(hipMemcpy(rinfo, d_info, b_info, hipMemcpyDeviceToHost));
+        HIPCHECK(hipMemcpy(accept, d_acc, b_acc, hipMemcpyDeviceToHost));
+        return 0;
+    };
+    rc = run();
+    (void)hipFree(d);
+    return rc;
 }

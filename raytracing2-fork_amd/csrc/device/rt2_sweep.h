@@ -66,6 +66,8 @@ struct RenderParams {
     const void* mfma_frag;       // MFMA: f16 filter records [group][quantity][lane][8] (rt2_mfma.h)
     const float* mfma_tau;       // MFMA: per-triangle record scale
     float mfma_A;                // MFMA: max |a_i| over the in-range triangles
+    const void* mfma_k16_frag;   // MFMA k16: f16 filter records [32-group][op][lane][8] (sweep_k16)
+    const float* mfma_k16_tau;   // MFMA k16: per-triangle record scale
     unsigned long long* wave_log;  // nullable diagnostic: per wave {start, pool dry, end, segments} (ASSIST)
     uint32_t wave_log_n;           // waves the log holds
 };

@@ -267,6 +267,8 @@ def lib() -> C.CDLL:
         "rt2_variant_name": (C.c_char_p, [C.c_int]),
         "rt2_scene_diag": (C.c_int, [P, C.POINTER(C.c_ulonglong), C.POINTER(C.c_int)]),
         "rt2_scene_plk_info": (C.c_int, [P, C.POINTER(C.c_int), C.POINTER(C.c_float), C.POINTER(C.c_int)]),
+        "rt2_scene_export": (C.c_longlong, [P, C.c_int, P, C.c_ulonglong]),
+        "rt2_mfma_probe": (C.c_int, [P, C.c_int, P, I32, P, P, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -578,6 +580,33 @@ class Scene:
         if not is_root:
             return None
         return (out, out8) if rgb8 else out
+
+    def export(self, what: int, dtype) -> np.ndarray:
+        """A derived device array of the scene (rt2_scene_export, test hook): 0 =
+        pre-transformed triangles, 1/2 = render_mfma records/tau, 3/4 = sweep_k16 records/tau."""
+        n = lib().rt2_scene_export(self._p, what, None, 0)
+        if n < 0:
+            raise RT2Error("rt2_scene_export: bad argument")
+        out = np.zeros(n // np.dtype(dtype).itemsize, dtype=dtype)
+        if n and lib().rt2_scene_export(self._p, what, out.ctypes.data, n) != n:
+            raise RT2Error("rt2_scene_export failed")
+        return out
+
+    def mfma_probe(self, layout: int, rays: np.ndarray):
+        """The matrix filter's terms on the device (rt2_mfma_probe, test hook):
+        rays (n, 8) float32 {o, best, d, 0}, n a multiple of 64; layout 0 =
+        16x16x32 (render_mfma), 1 = k16.  Returns (terms [n, n_pad, 5], frags
+        [n, 48] float16, rinfo [n, 8], accept [n, n_tris] bool)."""
+        rays = np.ascontiguousarray(rays, dtype=np.float32)
+        n = rays.shape[0]
+        n_pad = -(-self.n_tris // (32 if layout == 1 else 16)) * (32 if layout == 1 else 16)
+        terms = np.zeros((n, n_pad, 5), dtype=np.float32)
+        frags = np.zeros((n, 48), dtype=np.uint16)
+        rinfo = np.zeros((n, 8), dtype=np.float32)
+        acc = np.zeros((n, self.n_tris), dtype=np.uint8)
+        _check(lib().rt2_mfma_probe(self._p, layout, rays.ctypes.data, n, terms.ctypes.data, frags.ctypes.data,
+                                    rinfo.ctypes.data, acc.ctypes.data), "rt2_mfma_probe")
+        return terms, frags.view(np.float16), rinfo, acc.astype(bool)
 
     def stats(self, reset: bool = False) -> Stats:
         s = Stats()

@@ -27,6 +27,7 @@ ap.add_argument("--frames", type=int, default=0)
 ap.add_argument("--traversal", default="brute", choices=["brute", "bvh"])
 ap.add_argument("--no-split", action="store_true", help="whole-pixel items for F > 1")
 ap.add_argument("--cost-order", type=int, default=-1, help="1/0: force most-expensive-first item order on/off")
+ap.add_argument("--no-check", default="", help="comma list of variants whose image is not compared (speed-of-light probes)")
 a = ap.parse_args()
 sd, spec = rt2.build_config_scene(a.config)
 W, H, R = a.width or spec.width, a.height or spec.height, a.rays or spec.rays
@@ -53,9 +54,8 @@ for rnd in range(a.rounds):
         img = scene.render_host(u, 0, F)
         times[v].append(time.perf_counter() - t)
         scene.stats(reset=True)
-        c = (C.c_ulonglong * 8)()
-        lv = C.c_int()
-        rt2.lib().rt2_scene_diag(scene._p, c, C.byref(lv))
+        c = (C.c_ulonglong * 32)()
+        rt2.lib().rt2_scene_diag_ex(scene._p, c, 32)
         if a.traversal == "bvh":
             diag[v] = dict(segments=c[1], tests_per_segment=c[2] / max(c[1], 1),
                            interior_visits_per_segment=c[3] / max(c[1], 1),
@@ -66,10 +66,16 @@ for rnd in range(a.rounds):
                            lane_survivors=c[5], frac_groups_exact=c[3] / c[2], exact_iters_per_group=c[4] / c[2],
                            lane_survivor_rate=c[5] / (c[2] * 64 * 4),
                            wave_end_spread_ms=(c[7] - c[6]) * 1e-5 if c[7] > c[6] else None)
+            tt = [c[9], c[10], c[11], c[12]]  # render_mfma diag: shader clocks per phase (advance, sweep, shade, tail)
+            if sum(tt):
+                diag[v]["clock_share"] = dict(zip(("advance", "sweep", "shade", "tail"),
+                                                  [round(x / sum(tt), 4) for x in tt]))
+                diag[v]["sweep_clocks_per_group"] = round(c[10] / c[2], 1)
         if rnd == 0:
             if ref is None:
                 ref = img
-            assert np.array_equal(img, ref), f"variant {v} differs"
+            if str(v) not in a.no_check.split(","):
+                assert np.array_equal(img, ref), f"variant {v} differs"
             sha[v] = hashlib.sha256(np.ascontiguousarray(img).tobytes()).hexdigest()[:16]
 st = scene.stats(reset=True)
 samples = W * H * R * F

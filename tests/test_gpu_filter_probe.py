@@ -1,0 +1,158 @@
+"""The matrix filter's exactness argument, measured on the hardware it depends on.
+
+render_mfma skips the reference's Moller-Trumbore test (compute.glsl:302-340)
+for every (ray, triangle) pair whose filter term exceeds T (rt2_mfma.h); the
+safety argument ("The matrix filter") assumes f16 x f16 products and
+an f32 accumulation within 31 * 2^-24 * sum|p| in any order.  Here the real
+v_mfma_f32_16x16x32_f16 (render_mfma's 16x16 form) and v_mfma_f32_32x32x16_f16
+(the k16 form) run on the exact operand fragments the product sweeps build
+(rt2_mfma_probe: same scales, LDS rows, records and instructions) over
+adversarial rays and triangles (tests/filter_probe_lib.py), and the terms are
+compared with a binary64 evaluation on the host:
+  - accumulation error vs the exact sum of the same f16 operands <= the
+    assumed bound (and the observed worst case is recorded);
+  - total error vs the ideal filter quantity well inside T;
+  - conservativeness end to end: every pair the reference accepts (the device's
+    mt_exact, bit-identical to the oracle) passes the filter.
+RT2_PROBE_OUT=<file> writes the measured statistics as JSON
+(profiles/r03_filter_probe.json).  Then a near-threshold scene (shared edges
+hit dead on, coplanar near-duplicate triangles, stacked planes 2e-6 apart so
+hits land near dst = 1e-6, grazing views) is rendered by every product
+matrix-filter variant and compared with the oracle bit for bit.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import filter_probe_lib as fpl
+from test_gpu_parity import assert_exact, oracle_mean
+
+pytestmark = pytest.mark.gpu
+
+KINDS = ["unit", "far", "tiny", "mixed"]
+_results = {}
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available()
+    torch.cuda.set_device(0)
+    return torch
+
+
+def _tri_array(rt2mod, V):
+    t = np.zeros(len(V), dtype=rt2mod.TRI_DTYPE)
+    t["a"][:, :3], t["b"][:, :3], t["c"][:, :3] = V[:, 0], V[:, 1], V[:, 2]
+    return t
+
+
+def _materials(rt2mod):
+    sd = rt2mod.SceneData()
+    sd.add_material(rt2mod.Material.diffuse((0.8, 0.8, 0.8)))
+    return sd.materials()
+
+
+@pytest.mark.parametrize("layout", [0, 1], ids=["f16x32", "k16"])
+@pytest.mark.parametrize("kind", KINDS)
+def test_filter_terms_on_hardware(rt2mod, torch_cuda, kind, layout):
+    rng = np.random.default_rng(100 + KINDS.index(kind))
+    V, rays = fpl.scene_and_rays(kind, rng)
+    scene = rt2mod.Scene(triangles=_tri_array(rt2mod, V), materials=_materials(rt2mod))
+    tri = scene.export(0, np.float32).reshape(-1, 12)[:len(V)]
+    coef, tau, ok = fpl.coefs(tri)
+    if layout == 0:
+        B = fpl.records_16x16(scene.export(1, np.uint16), len(V))
+        T_tau = scene.export(2, np.float32)
+    else:
+        B = fpl.records_k16(scene.export(3, np.uint16), len(V))
+        T_tau = scene.export(4, np.float32)
+    # the device's records are the host's coefficients split into f16 hi/lo slots
+    np.testing.assert_array_equal(T_tau[:len(V)], tau.astype(np.float32))
+    hi = (coef * tau[:, None, None]).astype(np.float32).astype(np.float16).astype(np.float64)
+    np.testing.assert_array_equal(B[:, :4, 0:27:3], hi[:, :4, :9])
+    terms, frags, rinfo, accept = scene.mfma_probe(layout, rays)
+    st, viol = fpl.analyse(terms, frags, rinfo, accept, B, coef, tau, rays, T_tau)
+    st["triangles_in_range"] = int(ok.sum())
+    _results[f"{kind}/{['f16x32', 'k16'][layout]}"] = st
+    assert st["rays_in_range"] >= len(rays) // 2
+    assert st["accepted_pairs"] > 0
+    assert st["violations"] == 0, f"reference-accepted pairs rejected by the filter: {viol[:10]}"
+    assert st["acc_err_max_in_2^-24_sum_abs"] <= st["acc_err_bound_assumed"], st
+    assert st["total_err_max_over_T"] < 0.5, st
+    # padding triangles never pass
+    n_pad = terms.shape[1]
+    if n_pad > len(V):
+        pad_bits = terms[rinfo[:, 0] == 1.0, len(V):, :].view(np.int32).max(-1)
+        Tl = (T_tau[None, len(V):] * rinfo[rinfo[:, 0] == 1.0, 2][:, None]).astype(np.float32)
+        assert (pad_bits > Tl.view(np.int32)).all()
+
+
+def test_write_probe_summary():
+    out = os.environ.get("RT2_PROBE_OUT")
+    if not out or not _results:
+        pytest.skip("RT2_PROBE_OUT not set")
+    summary = {
+        "what": "matrix-filter terms on gfx950 vs binary64 (tests/test_gpu_filter_probe.py)",
+        "T": "2^-12 (Omax + A + 1) sigma tau (MfmaSpec::tshift = 12)",
+        "worst": {
+            "acc_err_max_in_2^-24_sum_abs": max(v["acc_err_max_in_2^-24_sum_abs"] for v in _results.values()),
+            "total_err_max_over_T": max(v["total_err_max_over_T"] for v in _results.values()),
+            "violations": sum(v["violations"] for v in _results.values()),
+            "accepted_pairs": sum(v["accepted_pairs"] for v in _results.values()),
+            "accepted_within_T_of_a_boundary": sum(v["accepted_within_T_of_a_boundary"] for v in _results.values()),
+        },
+        "cases": _results,
+    }
+    os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
+    with open(out, "w") as f:
+        json.dump(summary, f, indent=1)
+
+
+def near_threshold_scene(rt2mod):
+    """Grazing and edge-on geometry around a light: a tessellated floor whose
+    shared edges and vertices fall on pixel rays, its coplanar near-duplicate
+    (1e-6 perturbed) copy, a stack of parallel plates 2e-6 apart (hits near
+    the dst <= 1e-6 cut after a bounce), and a wall seen almost edge-on."""
+    M = rt2mod.Material
+    sd = rt2mod.SceneData()
+    diff = sd.add_material(M.diffuse((0.8, 0.75, 0.7)))
+    light = sd.add_material(M.light((1, 1, 1), 6.0))
+    mirror = sd.add_material(M.specular((0.9, 0.9, 0.9), (1, 1, 1), 1.0, 1.0))
+    rng = np.random.default_rng(7)
+    tris = []
+    step = 0.5
+    for i in range(-6, 6):
+        for j in range(-6, 6):
+            x0, z0 = i * step, -4.0 + j * step
+            p = [(x0, 0.0, z0), (x0 + step, 0.0, z0), (x0 + step, 0.0, z0 + step), (x0, 0.0, z0 + step)]
+            tris.append((p[0], p[2], p[1], diff))
+            tris.append((p[0], p[3], p[2], diff))
+    dup = [(tuple(np.float32(np.array(a) + rng.normal(0, 1e-6, 3))), b, c, mirror) for a, b, c, _ in tris[::3]]
+    tris += dup
+    for k in range(4):  # stacked plates, 2e-6 apart
+        y = 1.0 + 2e-6 * k
+        tris.append(((-1.0, y, -3.0), (1.0, y, -3.0), (1.0, y, -1.0), diff if k % 2 else mirror))
+        tris.append(((-1.0, y, -3.0), (1.0, y, -1.0), (-1.0, y, -1.0), diff))
+    tris.append(((3.0, -1.0, -8.0), (3.0 + 1e-4, 6.0, -8.0), (3.0 + 2e-4, -1.0, 2.0), diff))  # wall almost edge-on
+    tris.append(((-2.0, 4.0, -5.0), (2.0, 4.0, -5.0), (0.0, 4.0, -2.0), light))
+    tris.append(((-2.0, 4.0, -5.0), (0.0, 4.0, -2.0), (2.0, 4.0, -5.0), light))
+    for a, b, c, m in tris:
+        sd.add_triangle(a, b, c, m)
+    return sd
+
+
+@pytest.mark.parametrize("variant", [150, 152, 160, 161, 162])
+def test_near_threshold_scene_bit_exact(rt2mod, oraclemod, torch_cuda, variant):
+    if not rt2mod.has_variant(variant):
+        pytest.skip(f"variant {variant} not in this build")
+    sd = near_threshold_scene(rt2mod)
+    u = rt2mod.offline_uniforms(64, 48, 8, 4, sd.num_triangles)
+    u.cameraPos.x, u.cameraPos.y, u.cameraPos.z = 0.0, 0.5, 4.0  # low over the floor: grazing rays
+    scene = rt2mod.Scene(sd, 0)
+    scene.set_variant(variant)
+    img = scene.render_host(u, 0, 2)
+    ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(48), 0, 2)
+    assert_exact(img, ref, f"near-threshold scene, variant {variant}")
