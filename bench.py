@@ -57,7 +57,8 @@ BVH_RECORD_BYTES = 64      # BVH: one child-pair record per interior visit (both
 BVH_TRI_BYTES = 48         # BVH: one pre-transformed triangle record per leaf test
 L2_PEAK_GBS = 34500.0      # MI355X_MICROARCH.md §L2: ≈34.5 TB/s aggregate
 MFMA_F16_PEAK_TFLOPS = 2500.0  # MI355X dense F16/BF16 matrix peak (MI355X_MICROARCH.md; no sparsity)
-MFMA_FLOP_PER_PAIR = 320   # render_mfma: 5 quantities x 32 k-slots x 2 per (ray, triangle) pair (rt2_mfma.h)
+MFMA_FLOP_PER_PAIR = 320   # render_mfma 16x16x32 form: 5 quantities x 32 k-slots x 2 per (ray, triangle) pair
+MFMA_K16_FLOP_PER_PAIR = 256  # the k16 sweep: 8 v_mfma_f32_32x32x16_f16 (32x32x16x2 FLOP each) per 1,024 pairs
 TARGET_RATIO = 10.0        # north star: >= 10x the CPU reference at config C on 1 GPU
 KERNEL_FILES = {"mfma": "render_mfma", "massist": "render_assist", "smem": "render_smem", "split": "render_split", "tiled": "render_tiled", "assist": "render_assist",
                 "resident": "render_resident", "bvh4": "render_bvh4", "bvh3": "render_bvh3", "bvh2": "render_bvh2",
@@ -204,12 +205,18 @@ def roofline(tests, visits, kern_ms, segments=0, n_tris=0, variant=None):
                                    "frac": round(hbm / HBM_PEAK_GBS, 3),
                                    "note": "36 B x tests; >1 = on-chip reuse (effective bandwidth)"}}
     if variant and variant.startswith(("mfma", "massist")) and segments and n_tris:
-        pairs = segments * (-(-int(n_tris) // 16) * 16)
-        mf = MFMA_FLOP_PER_PAIR * pairs / (kern_ms * 1e-3) / 1e12
+        k16 = "/k16/" in variant
+        group = 32 if k16 else 16
+        pairs = segments * (-(-int(n_tris) // group) * group)
+        fpp = MFMA_K16_FLOP_PER_PAIR if k16 else MFMA_FLOP_PER_PAIR
+        mf = fpp * pairs / (kern_ms * 1e-3) / 1e12
+        model = ("256 x (ray, triangle) pairs: the k16 sweep's 8 v_mfma_f32_32x32x16_f16 per 32 rays x 32 "
+                 "triangles (U, -V, X: two K-halves each; -tn, Y: one), triangles padded to 32"
+                 if k16 else "320 x (ray, triangle) pairs (5 f16x3 products of 32 k-slots per pair, triangles "
+                             "padded to 16)")
         rf.update({"bound": "mfma", "achieved": round(mf, 3), "peak": MFMA_F16_PEAK_TFLOPS,
                    "frac": round(mf / MFMA_F16_PEAK_TFLOPS, 4),
-                   "flop_model": "320 x (ray, triangle) pairs (5 f16x3 products of 32 k-slots per pair, triangles "
-                                 "padded to 16; rays = segments: the active lanes) on the matrix cores",
+                   "flop_model": model + "; rays = segments (the active lanes) on the matrix cores",
                    "valu_algorithmic": {"achieved": round(flops, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                                         "frac": round(flops / VALU_PEAK_TFLOPS, 4),
                                         "note": "53 FLOP x tests (the reference formulation) / kernel time: the "

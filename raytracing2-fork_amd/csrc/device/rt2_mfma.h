@@ -56,6 +56,12 @@ struct MfmaSpec {
     bool k16 = false;       // sweep_k16: v_mfma_f32_32x32x16_f16 on 32-triangle groups, 8 products per 32 rays
     bool afrag_lds = false; // k16: the ray fragments are re-read from LDS every group (fewer VGPRs)
     bool rsplit = false;    // k16: scheduling fence between the two 32-ray blocks (one block's terms live at a time)
+    bool lane_lds = false;  // k16: the lane's path state (all but o, d) waits in LDS during the sweep (fewer VGPRs)
+    bool compact = false;   // k16: <= 32 live rays move to lanes 0..31 and the second 32-ray block is skipped
+    int serial = 0;         // k16: scheduling fences per 32-ray block: 1 = U V X products | their max | -tn Y
+                            // products | the rest (48 accumulator VGPRs live); 2 = all 8 products | the reduction;
+                            // 3 = 1 without the fence between the blocks; 4 = 3 without the fence at the group end
+    int tile_groups = 0;    // k16 (render_mfma_tiled): 32-triangle groups per LDS record tile shared by the workgroup
     int sol = 0;            // speed-of-light probes (WRONG images; diag clocks only): 1 = every group reads group
                             // 0's records, 2 = no exact phase, 3 = 2 + only the U term is reduced
 };
@@ -441,6 +447,61 @@ struct MfmaK16Lds {
     // (112-B rows: 16-B reads of 16 consecutive rows hit distinct banks)
     _Float16 ray[64][56];
 };
+// MfmaSpec::lane_lds: the path state a lane does not need during the sweep,
+// field-major (one 256-B row per field: conflict-free)
+constexpr int kLaneStash = 20;
+struct MfmaK16LaneLds : MfmaK16Lds {
+    uint32_t lane[kLaneStash][64];
+};
+__device__ __forceinline__ void lane_stash(const Lane& L, uint32_t (*st)[64], int l) {
+    const uint32_t v[kLaneStash] = {(uint32_t)L.st, L.item, (uint32_t)L.x, (uint32_t)L.y, L.frame, L.seed,
+                                    (uint32_t)L.ray, (uint32_t)L.bounce, (uint32_t)L.inside,
+                                    __float_as_uint(L.rayColor.x), __float_as_uint(L.rayColor.y),
+                                    __float_as_uint(L.rayColor.z), __float_as_uint(L.incoming.x),
+                                    __float_as_uint(L.incoming.y), __float_as_uint(L.incoming.z),
+                                    __float_as_uint(L.colorCum.x), __float_as_uint(L.colorCum.y),
+                                    __float_as_uint(L.colorCum.z), L.segs, L.t0};
+#pragma unroll
+    for (int f = 0; f < kLaneStash; f++) st[f][l] = v[f];
+}
+// ds_permute of a lane's whole path state to lane to/4 (push; a permutation)
+__device__ __forceinline__ int perm_i(int to, int v) { return __builtin_amdgcn_ds_permute(to, v); }
+__device__ __forceinline__ float perm_f(int to, float v) { return __int_as_float(__builtin_amdgcn_ds_permute(to, __float_as_int(v))); }
+__device__ __forceinline__ f3 perm_f3(int to, const f3& v) { return mk(perm_f(to, v.x), perm_f(to, v.y), perm_f(to, v.z)); }
+__device__ __forceinline__ void lane_permute(Lane& L, int to) {
+    L.st = perm_i(to, L.st);
+    L.item = (uint32_t)perm_i(to, (int)L.item);
+    L.x = perm_i(to, L.x);
+    L.y = perm_i(to, L.y);
+    L.frame = (uint32_t)perm_i(to, (int)L.frame);
+    L.seed = (uint32_t)perm_i(to, (int)L.seed);
+    L.ray = perm_i(to, L.ray);
+    L.bounce = perm_i(to, L.bounce);
+    L.inside = perm_i(to, (int)L.inside) != 0;
+    L.o = perm_f3(to, L.o);
+    L.d = perm_f3(to, L.d);
+    L.rayColor = perm_f3(to, L.rayColor);
+    L.incoming = perm_f3(to, L.incoming);
+    L.colorCum = perm_f3(to, L.colorCum);
+    L.segs = (uint32_t)perm_i(to, (int)L.segs);
+    L.t0 = (uint32_t)perm_i(to, (int)L.t0);
+}
+__device__ __forceinline__ void lane_unstash(Lane& L, const uint32_t (*st)[64], int l) {
+    L.st = (int)st[0][l];
+    L.item = st[1][l];
+    L.x = (int)st[2][l];
+    L.y = (int)st[3][l];
+    L.frame = st[4][l];
+    L.seed = st[5][l];
+    L.ray = (int)st[6][l];
+    L.bounce = (int)st[7][l];
+    L.inside = st[8][l] != 0;
+    L.rayColor = mk(__uint_as_float(st[9][l]), __uint_as_float(st[10][l]), __uint_as_float(st[11][l]));
+    L.incoming = mk(__uint_as_float(st[12][l]), __uint_as_float(st[13][l]), __uint_as_float(st[14][l]));
+    L.colorCum = mk(__uint_as_float(st[15][l]), __uint_as_float(st[16][l]), __uint_as_float(st[17][l]));
+    L.segs = st[18][l];
+    L.t0 = st[19][l];
+}
 
 __global__ void prep_mfma_k16(const float4* tri, int n, int n_pad, _Float16* out, float* tau_out, uint32_t* flags) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -479,7 +540,9 @@ __device__ __forceinline__ K16Terms k16_terms(const h8& a0, const h8& a1, const 
 
 template <MfmaSpec S>
 __device__ __forceinline__ bool sweep_k16(const RenderParams& p, MfmaK16Lds& sh, const f3& o, const f3& d, float& best,
-                                          int& bi, float& bestK, MfmaDiag& dg) {
+                                          int& bi, float& bestK, MfmaDiag& dg, bool upper = true) {
+    // upper = false: lanes 32..63 carry no ray of their own (MfmaSpec::compact moved the live rays to the
+    // low half), so the second 32-ray block's products and reduction are skipped
     static_assert(S.ymma && S.imax && S.minred, "the k16 sweep implements the ymma / imax / minred form");
     const int lane = (int)lane_id();
     const int r32 = lane & 31, hl = lane >> 5;
@@ -544,7 +607,37 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, MfmaK16Lds& sh,
         int tmin = 0x7fffffff;
 #pragma unroll
         for (int R = 0; R < 2; R++) {
+            if (R == 1 && !upper) break;
+            if constexpr (S.serial == 1 || S.serial == 3 || S.serial == 4) {
+                const f16v zero = {};
+                f16v U = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[R], b[0], zero, 0, 0, 0);
+                f16v V = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[R], b[2], zero, 0, 0, 0);
+                f16v X = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[R], b[4], zero, 0, 0, 0);
+                U = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[R], b[1], U, 0, 0, 0);
+                V = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[R], b[3], V, 0, 0, 0);
+                X = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[R], b[5], X, 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                int t3[16];
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    t3[i] = max(max(__float_as_int(U[i]), __float_as_int(V[i])), __float_as_int(X[i]));
+                __builtin_amdgcn_sched_barrier(0);
+                const f16v T = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[R], b[6], zero, 0, 0, 0);
+                const f16v Y = __builtin_amdgcn_mfma_f32_32x32x16_f16(y1[R], b[6], zero, 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    tmin = min(tmin, max(max(t3[i], __float_as_int(T[i])), __float_as_int(Y[i])));
+                // serial 3: block R's last reduction may overlap block R+1's products;
+                // serial 4: and the next group's record loads may move up
+                if constexpr (S.serial == 1) __builtin_amdgcn_sched_barrier(0);
+                if constexpr (S.serial == 3) {
+                    if (R == 1) __builtin_amdgcn_sched_barrier(0);
+                }
+                continue;
+            }
             const K16Terms q = k16_terms(a0[R], a1[R], y1[R], b);
+            if constexpr (S.serial == 2) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int i = 0; i < 16; i++) {
                 // max of the five terms on their bit patterns (see sweep_mfma)
@@ -556,15 +649,62 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, MfmaK16Lds& sh,
                     tmin = min(tmin, t);
                 }
             }
-            if constexpr (S.rsplit) __builtin_amdgcn_sched_barrier(0);
+            if constexpr (S.rsplit || S.serial == 2) __builtin_amdgcn_sched_barrier(0);
         }
-        const unsigned long long M = S.sol >= 2 ? (unsigned long long)(tmin == 0x7ffffffe) : __ballot(tmin <= __float_as_int(Tl));
+        if constexpr (S.sol == 5) {
+            // marginal-cost probe: the products and the reduction once more (a
+            // runtime-zero accumulator keeps the compiler from reusing them)
+            f16v ez = {};
+            ez[0] = p.mfma_A * 0.0f;
+            int tmin2 = 0x7fffffff;
+#pragma unroll
+            for (int R = 0; R < 2; R++) {
+                f16v U = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[R], b[0], ez, 0, 0, 0);
+                f16v V = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[R], b[2], ez, 0, 0, 0);
+                f16v X = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[R], b[4], ez, 0, 0, 0);
+                U = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[R], b[1], U, 0, 0, 0);
+                V = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[R], b[3], V, 0, 0, 0);
+                X = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[R], b[5], X, 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                int t3[16];
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    t3[i] = max(max(__float_as_int(U[i]), __float_as_int(V[i])), __float_as_int(X[i]));
+                __builtin_amdgcn_sched_barrier(0);
+                const f16v T = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[R], b[6], ez, 0, 0, 0);
+                const f16v Y = __builtin_amdgcn_mfma_f32_32x32x16_f16(y1[R], b[6], ez, 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    tmin2 = min(tmin2, max(max(t3[i], __float_as_int(T[i])), __float_as_int(Y[i])));
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            if (tmin2 == 0x12345677) best = -best;  // never (a sink)
+        }
+        const unsigned long long M = (S.sol == 2 || S.sol == 3) ? (unsigned long long)(tmin == 0x7ffffffe)
+                                                                 : __ballot(tmin <= __float_as_int(Tl));
         if constexpr (S.diag) dg.groups += 1;
         if (M) {
             if constexpr (S.diag) dg.hot += 1;
             // triangles of the group with a passing pair: the exact phase, in index order
             uint32_t m32 = (uint32_t)(M | M >> 32);
             const float bk0 = bestK;
+            if constexpr (S.sol == 4) {
+                // marginal-cost probe: the exact phase once more, on copies
+                uint32_t mm = m32;
+                float best2 = best, bestK2 = bestK;
+                int bi2 = bi;
+                while (mm) {
+                    const int t = __builtin_ctz(mm);
+                    mm &= mm - 1;
+                    const int idx = 32 * G + t;
+                    if (idx >= p.n_tris) break;
+                    cfloat* tp = (cfloat*)p.tri + 12 * idx;
+                    const MtQ qq = mt_quantities(o, d, ldc4(tp), ldc4(tp + 4), ldc4(tp + 8));
+                    if (mt_pass3(qq, bestK2)) mt_exact(qq, idx, best2, bi2, bestK2);
+                }
+                if (bi2 == -12345) best = -best;  // never (a sink)
+            }
             while (m32) {
                 const int t = __builtin_ctz(m32);
                 m32 &= m32 - 1;
@@ -588,6 +728,133 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, MfmaK16Lds& sh,
         }
     }
     return true;
+}
+
+// ---------------------------------------------------------------------------
+// The k16 sweep with workgroup-shared LDS record tiles (render_mfma_tiled;
+// scenes whose records outgrow the L2: config C's 100k and config E's 1M
+// triangles, 7 KiB of records per 32 triangles).  The workgroup's waves sweep
+// the same records in the same order, so each tile of tile_groups groups is
+// brought into LDS once per workgroup — by LDS-DMA (global_load_lds_dwordx4:
+// no VGPRs, coalesced 1-KiB pieces split across the waves), double-buffered so
+// that tile t+1 is in flight while tile t is swept — instead of once per wave
+// from L2/MALL: 1/NW of the record traffic.  One barrier per tile.  Every wave
+// of the workgroup runs the tile loop (its barriers) in every segment; only
+// waves with rays of their own in the filter's range compute (`sweeping`).
+// The arithmetic is sweep_k16's, term for term.
+template <MfmaSpec S>
+__device__ __forceinline__ bool sweep_k16_tiles(const RenderParams& p, MfmaK16Lds& sh, h8 (*tiles)[S.tile_groups * kK16Ops * 64],
+                                                float (*ttau)[(S.tile_groups * 32 + 63) / 64 * 64], const f3& o,
+                                                const f3& d, float& best, int& bi, float& bestK, MfmaDiag& dg,
+                                                bool sweeping) {
+    static_assert(S.ymma && S.imax && S.minred && S.k16 && S.tile_groups > 0, "k16 ymma/imax/minred form");
+    constexpr int K = S.tile_groups, NW = S.block / 64;
+    const int lane = (int)lane_id();
+    const int r32 = lane & 31, hl = lane >> 5, wave = (int)(threadIdx.x >> 6);
+    MfmaScale sc{0.0f, 0.0f, 0.0f};
+    h8 a0[2], a1[2], y1[2];
+    bool compute = false, in_range = true;
+    auto write_y = [&](float bkv) {
+        _Float16 s[16];
+        mfma_y_chunk(s, d, o, bkv, sc.sigma, sc.Bmax);
+        h8* row = reinterpret_cast<h8*>(&sh.ray[lane][32]);
+        row[0] = h8{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7]};
+        row[1] = h8{s[8], s[9], s[10], s[11], s[12], s[13], s[14], s[15]};
+    };
+    auto read_y = [&]() {
+#pragma unroll
+        for (int R = 0; R < 2; R++) y1[R] = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][32 + 8 * hl]);
+    };
+    if (sweeping) {
+        const f3 m = cross(d, o);
+        in_range = mfma_scale<S>(p.mfma_A, o, d, m, sc);
+        if (in_range) {
+            mfma_main_row(&sh.ray[lane][0], d, m, o, sc.sigma);
+            write_y(bestK);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int R = 0; R < 2; R++) {
+                a0[R] = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][8 * hl]);
+                a1[R] = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][16 + 8 * hl]);
+            }
+            read_y();
+            compute = true;
+        }
+    }
+    const int ng = (p.n_tris + 31) >> 5, nt = (ng + K - 1) / K;
+    const int n_tau = ng * 32;
+    const h8* gsrc = reinterpret_cast<const h8*>(p.mfma_k16_frag);
+    // LDS-DMA of tile t into buffer t&1: 1-KiB record pieces (a lane's 16 B
+    // land at base + 16 lane) and 256-B tau pieces, round-robin over the waves
+    auto issue = [&](int t) {
+        const int g0 = t * K, gn = min(K, ng - g0), pieces = gn * kK16Ops, tp = (gn * 32 + 63) / 64;
+        for (int pc = wave; pc < pieces + tp; pc += NW) {
+            if (pc < pieces) {
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(gsrc + ((size_t)g0 * kK16Ops + pc) * 64 + lane),
+                    (__attribute__((address_space(3))) void*)&tiles[t & 1][pc * 64], 16, 0, 0);
+            } else {
+                const int q = pc - pieces, idx = min(32 * g0 + 64 * q + lane, n_tau - 1);
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(p.mfma_k16_tau + idx),
+                                                 (__attribute__((address_space(3))) void*)&ttau[t & 1][64 * q], 4, 0,
+                                                 0);
+            }
+        }
+    };
+    issue(0);
+    for (int t = 0; t < nt; t++) {
+        __syncthreads();  // tile t has landed (every wave's DMA), every wave is done with tile t-1's buffer
+        if (t + 1 < nt) issue(t + 1);
+        if (!compute) continue;
+        const int gn = min(K, ng - t * K);
+        for (int gi = 0; gi < gn; gi++) {
+            const int G = t * K + gi;
+            h8 b[kK16Ops];
+#pragma unroll
+            for (int op = 0; op < kK16Ops; op++) b[op] = tiles[t & 1][(gi * kK16Ops + op) * 64 + lane];
+            const float Tl = ttau[t & 1][gi * 32 + r32] * sc.Tw;
+            int tmin = 0x7fffffff;
+#pragma unroll
+            for (int R = 0; R < 2; R++) {
+                const K16Terms q = k16_terms(a0[R], a1[R], y1[R], b);
+#pragma unroll
+                for (int i = 0; i < 16; i++) {
+                    const int t3 = max(max(__float_as_int(q.U[i]), __float_as_int(q.V[i])), __float_as_int(q.X[i]));
+                    tmin = min(tmin, max(max(t3, __float_as_int(q.T[i])), __float_as_int(q.Y[i])));
+                }
+            }
+            const unsigned long long M = __ballot(tmin <= __float_as_int(Tl));
+            if constexpr (S.diag) dg.groups += 1;
+            if (M) {
+                if constexpr (S.diag) dg.hot += 1;
+                uint32_t m32 = (uint32_t)(M | M >> 32);
+                const float bk0 = bestK;
+                while (m32) {
+                    const int tt = __builtin_ctz(m32);
+                    m32 &= m32 - 1;
+                    const int idx = 32 * G + tt;
+                    if (idx >= p.n_tris) break;
+                    if constexpr (S.diag) dg.exact += 1;
+                    cfloat* tp = (cfloat*)p.tri + 12 * idx;
+                    const MtQ qq = mt_quantities(o, d, ldc4(tp), ldc4(tp + 4), ldc4(tp + 8));
+                    if (mt_pass3(qq, bestK)) mt_exact(qq, idx, best, bi, bestK);
+                }
+                if (__ballot(bestK != bk0)) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    write_y(bestK);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    read_y();
+                }
+            }
+        }
+    }
+    return in_range;
 }
 
 // ---------------------------------------------------------------------------
@@ -702,7 +969,7 @@ __global__ __launch_bounds__(64) void mfma_probe_kernel(RenderParams p, const fl
 // rays leave the filter's range sweeps with the scalar-path filter instead.
 template <MfmaSpec S>
 __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves))) void render_mfma(RenderParams p) {
-    using WL = std::conditional_t<S.k16, MfmaK16Lds, MfmaWaveLds>;
+    using WL = std::conditional_t<S.k16, std::conditional_t<S.lane_lds, MfmaK16LaneLds, MfmaK16Lds>, MfmaWaveLds>;
     __shared__ WL wl[S.block / 64];
     WL& sh = wl[threadIdx.x >> 6];
     if constexpr (S.lds_pad > 0) {
@@ -723,7 +990,7 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
     };
     for (;;) {
         advance(L, p);
-        const unsigned long long act = __ballot(L.st == ST_TRACE);
+        unsigned long long act = __ballot(L.st == ST_TRACE);
         stamp(dg.t_advance);
         if constexpr (S.lockstep) {
             if (!__syncthreads_or(act != 0)) break;
@@ -756,6 +1023,22 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
             stamp(dg.t_tail);
             continue;
         }
+        bool upper = true;
+        if constexpr (S.compact) {
+            // at most 32 live rays: move them to lanes 0..31 (every lane's path
+            // state travels with it; lanes are interchangeable), so that the
+            // sweep runs the first 32-ray block only
+            if (__popcll(act) <= 32) {
+                if (act >> 32) {
+                    const uint32_t l = lane_id(), nl = (uint32_t)__popcll(act);
+                    const bool live = (act >> l) & 1ull;
+                    const int to = 4 * (int)(live ? lanes_below(act) : nl + lanes_below(~act));
+                    lane_permute(L, to);
+                    act = __ballot(L.st == ST_TRACE);
+                }
+                upper = false;
+            }
+        }
         // lanes without a ray carry the first live lane's (their passes add no triangle)
         const int j0 = __builtin_ctzll(act);
         const bool mine = L.st == ST_TRACE;
@@ -765,8 +1048,18 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
         float best = 1e38f, bestK = 1e38f * 1.0009765625f;
         int bi = -1;
         bool swept;
-        if constexpr (S.k16)
-            swept = sweep_k16<S>(p, sh, ro, rd, best, bi, bestK, dg);
+        if constexpr (S.k16 && S.lane_lds) {
+            // the path state waits in LDS (its registers are free during the sweep)
+            lane_stash(L, sh.lane, (int)lane_id());
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            swept = sweep_k16<S>(p, sh, ro, rd, best, bi, bestK, dg, upper);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const f3 lo = L.o, ld = L.d;
+            lane_unstash(L, sh.lane, (int)lane_id());
+            L.o = lo;
+            L.d = ld;
+        } else if constexpr (S.k16)
+            swept = sweep_k16<S>(p, sh, ro, rd, best, bi, bestK, dg, upper);
         else
             swept = sweep_mfma<S>(p, sh, ro, rd, best, bi, bestK, dg);
         if (!swept && mine)
@@ -785,6 +1078,97 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
             atomicAdd(p.seg_counter + 1, dg.groups);  // (wave, triangle group) sweeps
             atomicAdd(p.seg_counter + 2, dg.hot);     // ... with a passing pair
             atomicAdd(p.seg_counter + 3, dg.exact);   // (wave, triangle) exact tests
+            atomicAdd(p.seg_counter + 8, dg.t_advance);
+            atomicAdd(p.seg_counter + 9, dg.t_sweep);
+            atomicAdd(p.seg_counter + 10, dg.t_shade);
+            atomicAdd(p.seg_counter + 11, dg.t_tail);
+        }
+}
+
+// render_mfma with workgroup-shared LDS record tiles (sweep_k16_tiles): the
+// same lockstep segment loop, but every wave of the workgroup enters the tile
+// loop in every segment (its barriers), then the cooperative drain, the
+// scalar-path fallback and the shading as in render_mfma.
+template <MfmaSpec S>
+__global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves))) void render_mfma_tiled(RenderParams p) {
+    constexpr int K = S.tile_groups;
+    __shared__ MfmaK16Lds wl[S.block / 64];
+    __shared__ h8 tiles[2][K * kK16Ops * 64];
+    __shared__ float ttau[2][(K * 32 + 63) / 64 * 64];
+    MfmaK16Lds& sh = wl[threadIdx.x >> 6];
+    Lane L;
+    lane_init(L);
+    MfmaDiag dg;
+    unsigned long long tc = 0;
+    if constexpr (S.diag) tc = __builtin_amdgcn_s_memtime();
+    auto stamp = [&](unsigned long long& acc) {
+        if constexpr (S.diag) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            acc += t - tc;
+            tc = t;
+        }
+    };
+    for (;;) {
+        advance(L, p);
+        const unsigned long long act = __ballot(L.st == ST_TRACE);
+        stamp(dg.t_advance);
+        if (!__syncthreads_or(act != 0)) break;  // workgroup-uniform: every wave leaves together
+        const bool coop = act != 0 && __popcll(act) <= (unsigned)S.tail_lanes && __any(L.st == ST_DONE);
+        const bool sweeping = act != 0 && !coop;
+        const bool mine = L.st == ST_TRACE;
+        f3 ro = L.o, rd = L.d;
+        if (sweeping) {  // lanes without a ray carry the first live lane's (their passes add no triangle)
+            const int j0 = __builtin_ctzll(act);
+            const f3 o = mk(__shfl(L.o.x, j0), __shfl(L.o.y, j0), __shfl(L.o.z, j0));
+            const f3 dd = mk(__shfl(L.d.x, j0), __shfl(L.d.y, j0), __shfl(L.d.z, j0));
+            ro = mine ? L.o : o;
+            rd = mine ? L.d : dd;
+        }
+        float best = 1e38f, bestK = 1e38f * 1.0009765625f;
+        int bi = -1;
+        const bool swept = sweep_k16_tiles<S>(p, sh, tiles, ttau, ro, rd, best, bi, bestK, dg, sweeping);
+        stamp(dg.t_sweep);
+        if (coop) {
+            float mybest = 1e38f;
+            int mybi = -1;
+            unsigned long long mm = act;
+            while (mm) {
+                const int j = __builtin_ctzll(mm);
+                mm &= mm - 1;
+                const f3 oj = mk(__shfl(L.o.x, j), __shfl(L.o.y, j), __shfl(L.o.z, j));
+                const f3 dj = mk(__shfl(L.d.x, j), __shfl(L.d.y, j), __shfl(L.d.z, j));
+                float b;
+                int bidx;
+                coop_closest(oj, dj, p.tri, p.n_tris, b, bidx);
+                if ((int)lane_id() == j) {
+                    mybest = b;
+                    mybi = bidx;
+                }
+            }
+            if (mine) {
+                L.bounce += 1;
+                L.segs += 1;
+                shade(L, p, mybest, mybi);
+            }
+            stamp(dg.t_tail);
+            continue;
+        }
+        if (!act) continue;
+        if (!swept && mine)
+            sweep_masked<8, true, Filter::Max3>(ro, rd, nullptr, (const float*)p.tri, p.n_tris, 0, best, bi, bestK);
+        if (mine) {
+            L.bounce += 1;
+            L.segs += 1;
+            shade(L, p, best, bi);
+        }
+        stamp(dg.t_shade);
+    }
+    flush_counters(L, p);
+    if constexpr (S.diag)
+        if (lane_id() == 0) {
+            atomicAdd(p.seg_counter + 1, dg.groups);
+            atomicAdd(p.seg_counter + 2, dg.hot);
+            atomicAdd(p.seg_counter + 3, dg.exact);
             atomicAdd(p.seg_counter + 8, dg.t_advance);
             atomicAdd(p.seg_counter + 9, dg.t_sweep);
             atomicAdd(p.seg_counter + 10, dg.t_shade);

@@ -541,11 +541,18 @@ constexpr MfmaSpec k16_spec(int waves, bool afrag_lds = false, bool diag = false
                     .minred = true, .diag = diag, .ymma = true, .tshift = 12, .k16 = true, .afrag_lds = afrag_lds,
                     .rsplit = rsplit};
 }
-constexpr MfmaSpec kMfmaT8Y4D{.block = 256, .waves = 4, .tail_lanes = 8, .imax = true, .minred = true, .diag = true,
-                              .ymma = true, .tshift = 12};
+constexpr MfmaSpec kMfmaK16 = [] {
+    MfmaSpec x = k16_spec(3);
+    x.lane_lds = true;
+    x.serial = 4;
+    x.compact = true;
+    return x;
+}();
 constexpr Bvh3Spec kBvhDefault{.block = 256, .thresh = 16, .slab = Slab::Markstein, .waves = 5, .diag = false};
 
 #ifdef RT2_EXPERIMENTS
+constexpr MfmaSpec kMfmaT8Y4D{.block = 256, .waves = 4, .tail_lanes = 8, .imax = true, .minred = true, .diag = true,
+                              .ymma = true, .tshift = 12};
 constexpr MfmaSpec kMfmaT8{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true};
 constexpr MfmaSpec kMfmaIM{.block = 256, .waves = 2, .tail_lanes = 16, .imax = true, .minred = true};
 constexpr MfmaSpec kMfmaT4{.block = 256, .waves = 2, .tail_lanes = 4, .imax = true, .minred = true};
@@ -596,6 +603,9 @@ const Variant kVariants[] = {
     RT2_VARIANT(152, K_MFMA, render_mfma<kMfmaT8Y4>, 256, "mfma/256/f16x3/coop8/w4/imax/minred/ymma/t12"),  // default (<= kMfmaMaxTris)
     RT2_VARIANT(150, K_MFMA, render_mfma<kMfmaT8Y>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma/t12"),  // 1.5-3 items per lane
     RT2_VARIANT(136, K_SMEM, render_smem<kSmemDefault>, 256, "smem/256/max3f8/coop32/w6/lockstep"),  // variant 0 forced (id 0 = automatic)
+    // default brute-force kernel for every scene in the matrix filter's range (DESIGN.md "The k16 sweep")
+    RT2_VARIANT(200, K_MFMA, render_mfma<kMfmaK16>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"),
+#ifdef RT2_EXPERIMENTS
     RT2_VARIANT(160, K_MFMA, render_mfma<k16_spec(3)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12"),
     RT2_VARIANT(161, K_MFMA, render_mfma<k16_spec(4)>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12"),
     RT2_VARIANT(162, K_MFMA, render_mfma<k16_spec(2)>, 256, "mfma/256/k16/coop8/w2/imax/minred/ymma/t12"),
@@ -611,10 +621,32 @@ const Variant kVariants[] = {
     RT2_VARIANT(190, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3, false, true); x.sol = 1; return x; }()>, 256, "SOL1/k16/w3/records-of-group-0"),
     RT2_VARIANT(191, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3, false, true); x.sol = 2; return x; }()>, 256, "SOL2/k16/w3/no-exact-phase"),
     RT2_VARIANT(192, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3, false, true); x.sol = 3; return x; }()>, 256, "SOL3/k16/w3/U-only"),
+    RT2_VARIANT(175, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3); x.lane_lds = true; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds"),
+    RT2_VARIANT(176, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3, false, false, false, true); x.lane_lds = true; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/pf/llds"),
+    RT2_VARIANT(177, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(4); x.lane_lds = true; return x; }()>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/llds"),
+    RT2_VARIANT(178, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(4, true); x.lane_lds = true; return x; }()>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/alds/llds"),
+    RT2_VARIANT(179, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(4, true); x.lane_lds = true; x.serial = 1; return x; }()>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/alds/llds/ser1"),
+    RT2_VARIANT(180, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(4, true); x.lane_lds = true; x.serial = 2; return x; }()>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/alds/llds/ser2"),
+    RT2_VARIANT(181, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3); x.serial = 1; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/ser1"),
+    RT2_VARIANT(182, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3); x.serial = 2; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/ser2"),
+    RT2_VARIANT(183, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(4); x.serial = 1; return x; }()>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/ser1"),
+    RT2_VARIANT(184, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3, false, false, false, true); x.lane_lds = true; x.serial = 1; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/pf/llds/ser1"),
+    RT2_VARIANT(185, K_MFMA, render_mfma_tiled<[] { MfmaSpec x = k16_spec(3); x.tile_groups = 1; return x; }()>, 256, "mfmat/256/k16/tile1/w3"),
+    RT2_VARIANT(186, K_MFMA, render_mfma_tiled<[] { MfmaSpec x = k16_spec(3); x.block = 768; x.tile_groups = 4; return x; }()>, 768, "mfmat/768/k16/tile4/w3"),
+    RT2_VARIANT(187, K_MFMA, render_mfma_tiled<[] { MfmaSpec x = k16_spec(3, false, true); x.block = 768; x.tile_groups = 4; return x; }()>, 768, "mfmat/768/k16/tile4/w3/diag"),
+    RT2_VARIANT(188, K_MFMA, render_mfma_tiled<[] { MfmaSpec x = k16_spec(3); x.block = 512; x.tile_groups = 2; return x; }()>, 512, "mfmat/512/k16/tile2/w3"),
+    RT2_VARIANT(189, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3); x.lane_lds = true; x.serial = 1; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser1"),
+    RT2_VARIANT(193, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3, true, false, false, true); x.lane_lds = true; x.serial = 1; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/alds/pf/llds/ser1"),
+    RT2_VARIANT(194, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3, true); x.serial = 1; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/alds/ser1"),
+    RT2_VARIANT(195, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3); x.lane_lds = true; x.serial = 1; x.sol = 4; return x; }()>, 256, "SOL4/k16/llds/ser1/exact-phase-twice"),
+    RT2_VARIANT(196, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3); x.lane_lds = true; x.serial = 1; x.sol = 5; return x; }()>, 256, "SOL5/k16/llds/ser1/products-and-reduction-twice"),
+    RT2_VARIANT(197, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3); x.lane_lds = true; x.serial = 3; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser3"),
+    RT2_VARIANT(198, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3); x.lane_lds = true; x.serial = 4; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser4"),
+    RT2_VARIANT(199, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(2); x.lane_lds = true; x.serial = 4; return x; }()>, 256, "mfma/256/k16/coop8/w2/imax/minred/ymma/t12/llds/ser4"),
+    RT2_VARIANT(201, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3); x.lane_lds = true; x.serial = 1; x.compact = true; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser1/cmp"),
     RT2_VARIANT(166, K_MFMA, render_mfma<k16_spec(3, false, false, true)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/rsplit"),
     RT2_VARIANT(167, K_MFMA, render_mfma<k16_spec(4, true, false, true)>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/alds/rsplit"),
     RT2_VARIANT(168, K_MFMA, render_mfma<k16_spec(3, true, false, true)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/alds/rsplit"),
-#ifdef RT2_EXPERIMENTS
     RT2_VARIANT(140, K_MFMA, render_mfma<kMfmaT8>, 256, "mfma/256/f16x3/coop8/w2/imax/minred"),  // Y by one FMA per pair
     RT2_VARIANT(137, K_MFMA, render_mfma<kMfmaIM>, 256, "mfma/256/f16x3/coop16/w2/imax/minred"),  // drain at 16 live rays
     RT2_VARIANT(143, K_MFMA, render_mfma<kMfmaT4>, 256, "mfma/256/f16x3/coop4/w2/imax/minred"),
@@ -696,11 +728,9 @@ constexpr int kDefaultBrute = 0;
 constexpr int kDefaultBvh = 109;
 constexpr int kLargeScene = 86;  // tiled/512/max3f4: LDS tiles above kSmemMaxTris triangles
 constexpr int kSlab = 92;        // assist12/max3f8/w6: fewer than 4 items per lane (multi-GPU slabs)
-constexpr int kMfma = 152;       // mfma/.../coop8/w4/imax/minred/ymma: matrix-core filter (config B: 287 vs 530 ms)
-constexpr int kMfmaMid = 150;    // the same at 3 waves per SIMD (1.5 to 3 items per 4-wave lane; large scenes)
-constexpr int kMfma4MaxTris = 8192;  // 4 waves only while the records (5 KiB per 16 triangles) fit an XCD's L2
-constexpr int kMfmaMaxTris = kSmemMaxTris;  // 41 MiB of f16 records; config C (100k triangles, 480x270x2 frames
-                                           // sample): 4.9 vs 8.3 s for render_smem
+constexpr int kMfma = 200;  // mfma/.../k16/...: the matrix-core filter on v_mfma_f32_32x32x16_f16 (DESIGN.md "The k16
+                            // sweep"): config B 256 vs 283 ms for the 16x16x32 form (variant 152), config C sample
+                            // 2.13 vs 2.43 s, config E sample 3.9 vs 6.9 s for the scalar LDS-tiled kernel
 
 constexpr bool is_bvh(int kind) { return kind >= K_BVH && kind <= K_BVH4; }
 
@@ -938,7 +968,14 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     if (!VP && s->traversal == RT2_TRAVERSAL_BVH) VP = find_variant(kDefaultBvh);
     if (!VP) {
         int vi = s->n_tris <= kSmemMaxTris ? kDefaultBrute : kLargeScene;
-        if (vi == kDefaultBrute) {
+        if (s->mfma_ok && find_variant(kMfma)) {
+            // the filter on the matrix cores (rt2_mfma.h) for whole images and
+            // rank slabs alike (its compaction of <= 32 live rays serves the
+            // slabs' tails) and every scene size: config E's 1M triangles too
+            // (3.9 vs 6.9 s for kLargeScene on a 480x270 sample)
+            vi = kMfma;
+        } else if (vi == kDefaultBrute) {
+            // scenes outside the matrix filter's range (mfma_ok = 0):
             // items per resident lane decide the tail: a lane ends on a whole
             // item (a pixel-frame's rays share one RNG stream), so with few
             // items per lane the last round runs partly empty.  At >= 4 per
@@ -950,20 +987,7 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
             int occ0 = 0;
             HIPCHECK(variant_occupancy(*W, &occ0, 0));
             const unsigned long long lanes = (unsigned long long)s->num_cus * (unsigned long long)std::max(occ0, 1) * W->block;
-            if (s->mfma_ok && s->n_tris <= kMfmaMaxTris && find_variant(kMfma) && find_variant(kMfmaMid)) {
-                // the filter on the matrix cores (rt2_mfma.h; DESIGN.md "The matrix filter"): whole
-                // config B 276 vs 530 ms, its 1/2, 1/4, 1/8 slabs 152 / 77 / 42 ms vs 267 / 143 / 76 for
-                // the assist kernel.  4 waves per SIMD while the records stay in an XCD's L2, except at
-                // 1.5 to 3 items per 4-wave lane (the 1/4 slab: 1.98), where the 3-wave build's last
-                // round is fuller (80 vs 83 ms); 3 waves for larger scenes, whose records stream from
-                // the MALL (config C sample: 2.39 vs 3.02 s)
-                int occ4 = 0;
-                HIPCHECK(variant_occupancy(*find_variant(kMfma), &occ4, 0));
-                const double ipl = (double)p.n_items /
-                                   ((double)s->num_cus * (double)std::max(occ4, 1) * find_variant(kMfma)->block);
-                vi = (s->n_tris > kMfma4MaxTris || (ipl >= 1.5 && ipl < 3.0)) ? kMfmaMid : kMfma;
-            } else if (p.n_items < 4 * lanes)
-                vi = kSlab;
+            if (p.n_items < 4 * lanes) vi = kSlab;
         }
         VP = find_variant(vi);
     }

@@ -11,4 +11,7 @@ timeout -k 10 240 python scripts/ab_variants.py --config B --no-check "${NOCHECK
 if [ -n "${CVARIANTS}" ]; then
   timeout -k 10 300 python scripts/ab_variants.py --config C --width 480 --height 270 --frames 2 --no-check "${NOCHECK}" --variants ${CVARIANTS} --rounds 2 > gpurun_out/ab_C.json 2>&1 || { echo "ab C failed"; exit 1; }
 fi
+if [ -n "${SVARIANTS}" ]; then
+  timeout -k 10 200 python scripts/shard_probe.py --variants ${SVARIANTS} > gpurun_out/shard_ab.log 2>&1 || { echo "shard probe failed"; exit 1; }
+fi
 echo "all ok"

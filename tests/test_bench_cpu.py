@@ -94,6 +94,10 @@ def test_roofline_matrix_kernel():
     # other kernels keep the VALU roofline even when given segments
     assert bench.roofline(segs * n, 0, kern_ms, segs, n, "smem/x")["bound"] == "valu"
     assert bench.kernel_label("mfma/256/f16x3/coop16/w2/imax").startswith("render_mfma")
+    # the k16 sweep: 256 FLOP per pair over triangles padded to 32
+    rf = bench.roofline(segs * n, 0, kern_ms, segs, n, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp")
+    assert rf["achieved"] == pytest.approx(bench.MFMA_K16_FLOP_PER_PAIR * segs * 1216 / (kern_ms * 1e-3) / 1e12,
+                                           rel=1e-3)
 
 
 def test_kernel_labels():

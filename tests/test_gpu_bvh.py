@@ -189,14 +189,20 @@ def test_bvh2_big_leaves_and_single_node(rt2mod, oraclemod, torch_cuda):
 
 
 @pytest.mark.parametrize("traversal", ["brute", "bvh"])
-def test_config_E_million_triangles(rt2mod, oraclemod, config_scene, torch_cuda, traversal):
+@pytest.mark.parametrize("brute_variant", [0, 86], ids=["auto-k16", "tiled"])
+def test_config_E_million_triangles(rt2mod, oraclemod, config_scene, torch_cuda, traversal, brute_variant):
     """Config E (1,000,014 triangles, mirror box, 16 bounces) at a small image:
-    both traversals bit-exact against the oracle (brute: the tiled kernel)."""
+    both traversals bit-exact against the oracle; brute force by the automatic
+    choice (the k16 matrix kernel, variant 200) and the scalar LDS-tiled kernel."""
+    if traversal == "bvh" and brute_variant:
+        pytest.skip("the brute-force variant does not apply to the BVH traversal")
     sd, spec = config_scene("E")
     W, H = (12, 8) if traversal == "brute" else (48, 32)
     u = rt2mod.offline_uniforms(W, H, spec.bounces, 2, sd.num_triangles)
     scene = rt2mod.Scene(sd, 0)
     scene.set_traversal(traversal)
+    if brute_variant:
+        scene.set_variant(brute_variant)
     img = scene.render_host(u, 0, 1)
     st = scene.stats(reset=True)
     ref, _, segs = oracle_mean(oraclemod, sd, u, np.arange(H), 0, 1, traversal)

@@ -18,7 +18,19 @@ MFMA = 150
 # per pair, record prefetch, 4 waves/SIMD, other drain thresholds,
 # free-running waves and the assist kernel with the matrix filter (138, 139:
 # forced here, so every segment with helpers is a job of group-range units)
-VARIANTS = [150, 152, 160, 161, 162, 163, 164, 166, 167, 168, 170, 171, 172, 173] + ([130, 131, 132, 133, 134, 135, 137, 138, 139, 140, 143, 144, 145, 146, 147, 148, 149, 151, 153, 154, 155, 156, 157, 158, 159] if EXPERIMENTS else [])
+def _mfma_variants():
+    """Every matrix-filter variant the loaded library carries (ids 130-259),
+    except the timing-only speed-of-light probes."""
+    import rt2
+    out = []
+    for v in range(130, 260):
+        name = rt2.lib().rt2_variant_name(v)
+        if name and name.decode().startswith(("mfma", "massist")):
+            out.append(v)
+    return out
+
+
+VARIANTS = _mfma_variants()
 
 
 @pytest.fixture(params=VARIANTS, ids=lambda v: f"v{v}")

@@ -100,19 +100,17 @@ def _last_variant(rt2mod, scene):
     return rt2mod.lib().rt2_variant_name(lv.value).decode()
 
 
-AUTO_MFMA = "mfma/256/f16x3/coop8/w4/imax/minred/ymma/t12"  # variant 152 (4 waves per SIMD)
-AUTO_MFMA_MID = "mfma/256/f16x3/coop8/w2/imax/minred/ymma/t12"  # variant 150: 1.5-3 items per 4-wave lane
+AUTO_MFMA = "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"  # variant 200 (the k16 sweep)
 
 
 def test_auto_variant_large_scene(rt2mod, config_scene, torch_cuda):
     """Scenes whose matrix-filter records outgrow an XCD's L2 (config C: 100k
-    triangles, 31 MB) run the 3-wave build whatever the items per lane
-    (config C sample: 2.39 vs 3.02 s at 4 waves)."""
+    triangles, 22 MB of k16 records) run the same k16 matrix kernel."""
     sd, spec = config_scene("C")
     u = rt2mod.offline_uniforms(64, 36, spec.bounces, 1, sd.num_triangles)
     scene = rt2mod.Scene(sd, 0)
     scene.render_host(u, 0, 1)
-    assert _last_variant(rt2mod, scene) == AUTO_MFMA_MID
+    assert _last_variant(rt2mod, scene) == AUTO_MFMA
 
 
 def test_auto_variant_by_items_per_lane(rt2mod, config_scene, torch_cuda):
@@ -125,7 +123,7 @@ def test_auto_variant_by_items_per_lane(rt2mod, config_scene, torch_cuda):
     scene = rt2mod.Scene(sd, 0)
     full = scene.render_host(u, 0, 1)
     assert _last_variant(rt2mod, scene) == AUTO_MFMA
-    for n, want in ((2, AUTO_MFMA), (4, AUTO_MFMA_MID), (8, AUTO_MFMA)):
+    for n, want in ((2, AUTO_MFMA), (4, AUTO_MFMA), (8, AUTO_MFMA)):
         sh = rt2mod.shard(1, n - 1, n)
         img = scene.render_host(u, 0, 1, sh)
         assert _last_variant(rt2mod, scene) == want
@@ -305,11 +303,11 @@ def test_frame_split_identical(rt2mod, oraclemod, config_scene, torch_cuda, trav
 
 
 # brute-force kernel variants that change the schedule, not the arithmetic:
-# the product variants (0 = automatic, 86, 92, 150/152 = the matrix filter, 136 = the scalar path
+# the product variants (0 = automatic, 86, 92, 150/152/200 = the matrix filter, 136 = the scalar path
 # forced) and, in an experiment build, the A/B
 # variants (masked/plk filters, resident LDS, cooperative and team tail modes,
 # split waves, the round-1 slab kernels, occupancy hints)
-BRUTE_VARIANTS = [0, 86, 92, 150, 152, 136] + ([137, 138, 139, 140, 143, 144, 145, 146] if EXPERIMENTS else []) + ([22, 24, 28, 52, 64, 65, 66, 67, 68, 70, 71, 72, 73, 74, 76, 79, 80, 84, 85, 87, 89, 95, 97, 101, 104, 106,
+BRUTE_VARIANTS = [0, 86, 92, 150, 152, 200, 136] + ([137, 138, 139, 140, 143, 144, 145, 146] if EXPERIMENTS else []) + ([22, 24, 28, 52, 64, 65, 66, 67, 68, 70, 71, 72, 73, 74, 76, 79, 80, 84, 85, 87, 89, 95, 97, 101, 104, 106,
                                  90] if EXPERIMENTS else [])
 
 
