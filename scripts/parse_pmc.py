@@ -14,7 +14,7 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-OUT = os.path.join(ROOT, "gpurun_out")
+OUT = os.environ.get("PMC_DIR", os.path.join(ROOT, "gpurun_out"))
 sys.path.insert(0, ROOT)
 from bench import kernel_source_digest  # noqa: E402
 
