@@ -56,7 +56,10 @@ struct MfmaSpec {
     bool k16 = false;       // sweep_k16: v_mfma_f32_32x32x16_f16 on 32-triangle groups, 8 products per 32 rays
     bool afrag_lds = false; // k16: the ray fragments are re-read from LDS every group (fewer VGPRs)
     bool rsplit = false;    // k16: scheduling fence between the two 32-ray blocks (one block's terms live at a time)
-    bool lane_lds = false;  // k16: the lane's path state (all but o, d) waits in LDS during the sweep (fewer VGPRs)
+    int lane_lds = 0;       // k16: the lane's path state (all but o, d) waits in LDS during the sweep (fewer VGPRs);
+                            // 2 = packed into 16 words with 96-B fragment rows (10 KiB of LDS per wave: 4 waves/SIMD)
+    bool lateload = false;  // k16 (serial 1/3/4): the next group's records are requested into the operand registers
+                            // right after this group's last product is issued (no extra VGPRs)
     bool compact = false;   // k16: <= 32 live rays move to lanes 0..31 and the second 32-ray block is skipped
     int serial = 0;         // k16: scheduling fences per 32-ray block: 1 = U V X products | their max | -tn Y
                             // products | the rest (48 accumulator VGPRs live); 2 = all 8 products | the reduction;
@@ -486,6 +489,41 @@ __device__ __forceinline__ void lane_permute(Lane& L, int to) {
     L.segs = (uint32_t)perm_i(to, (int)L.segs);
     L.t0 = (uint32_t)perm_i(to, (int)L.t0);
 }
+// lane_lds = 2: 15 words (st:3 inside:1 bounce:12 ray:16 | item | x:16 y:16 |
+// frame | seed | colours | segs; t0 keeps its register); the launcher uses it
+// only when bounce <= 4095, rays per pixel <= 65535 and the image fits 16-bit
+// coordinates
+struct MfmaK16PackedLds {
+    _Float16 ray[64][48];  // 96-B rows (two-way bank conflicts on the per-segment fragment reads)
+    uint32_t lane[15][64];
+};
+__device__ __forceinline__ void lane_stash_packed(const Lane& L, uint32_t (*st)[64], int l) {
+    const uint32_t v[15] = {(uint32_t)L.st | (uint32_t)L.inside << 3 | (uint32_t)L.bounce << 4 | (uint32_t)L.ray << 16,
+                            L.item, (uint32_t)L.x | (uint32_t)L.y << 16, L.frame, L.seed,
+                            __float_as_uint(L.rayColor.x), __float_as_uint(L.rayColor.y),
+                            __float_as_uint(L.rayColor.z), __float_as_uint(L.incoming.x),
+                            __float_as_uint(L.incoming.y), __float_as_uint(L.incoming.z),
+                            __float_as_uint(L.colorCum.x), __float_as_uint(L.colorCum.y),
+                            __float_as_uint(L.colorCum.z), L.segs};
+#pragma unroll
+    for (int f = 0; f < 15; f++) st[f][l] = v[f];
+}
+__device__ __forceinline__ void lane_unstash_packed(Lane& L, const uint32_t (*st)[64], int l) {
+    const uint32_t w = st[0][l], xy = st[2][l];
+    L.st = (int)(w & 7u);
+    L.inside = ((w >> 3) & 1u) != 0;
+    L.bounce = (int)((w >> 4) & 0xfffu);
+    L.ray = (int)(w >> 16);
+    L.item = st[1][l];
+    L.x = (int)(xy & 0xffffu);
+    L.y = (int)(xy >> 16);
+    L.frame = st[3][l];
+    L.seed = st[4][l];
+    L.rayColor = mk(__uint_as_float(st[5][l]), __uint_as_float(st[6][l]), __uint_as_float(st[7][l]));
+    L.incoming = mk(__uint_as_float(st[8][l]), __uint_as_float(st[9][l]), __uint_as_float(st[10][l]));
+    L.colorCum = mk(__uint_as_float(st[11][l]), __uint_as_float(st[12][l]), __uint_as_float(st[13][l]));
+    L.segs = st[14][l];
+}
 __device__ __forceinline__ void lane_unstash(Lane& L, const uint32_t (*st)[64], int l) {
     L.st = (int)st[0][l];
     L.item = st[1][l];
@@ -538,8 +576,8 @@ __device__ __forceinline__ K16Terms k16_terms(const h8& a0, const h8& a1, const 
     return r;
 }
 
-template <MfmaSpec S>
-__device__ __forceinline__ bool sweep_k16(const RenderParams& p, MfmaK16Lds& sh, const f3& o, const f3& d, float& best,
+template <MfmaSpec S, class SH>
+__device__ __forceinline__ bool sweep_k16(const RenderParams& p, SH& sh, const f3& o, const f3& d, float& best,
                                           int& bi, float& bestK, MfmaDiag& dg, bool upper = true) {
     // upper = false: lanes 32..63 carry no ray of their own (MfmaSpec::compact moved the live rays to the
     // low half), so the second 32-ray block's products and reduction are skipped
@@ -589,8 +627,12 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, MfmaK16Lds& sh,
         tg += 32;
     };
     if constexpr (S.prefetch) fetch(nb, ntau);
+    if constexpr (S.lateload) fetch(b, tau);
     for (int G = 0; G < ng; G++) {
-        if constexpr (S.prefetch) {
+        if constexpr (S.lateload) {
+            // b, tau arrived during the previous group (requested right after
+            // its last product was issued)
+        } else if constexpr (S.prefetch) {
             // this group's records arrived during the previous group's
             // products; the next group's are requested before this group's
 #pragma unroll
@@ -625,6 +667,15 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, MfmaK16Lds& sh,
                 const f16v T = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[R], b[6], zero, 0, 0, 0);
                 const f16v Y = __builtin_amdgcn_mfma_f32_32x32x16_f16(y1[R], b[6], zero, 0, 0, 0);
                 __builtin_amdgcn_sched_barrier(0);
+                if constexpr (S.lateload) {
+                    // the group's last product is issued: its operand registers
+                    // take the next group's records, whose latency the rest of
+                    // this group (reduction, ballot, exact phase) covers
+                    if (R == 1 || !upper) {
+                        if (G + 1 < ng) fetch(b, tau);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                }
 #pragma unroll
                 for (int i = 0; i < 16; i++)
                     tmin = min(tmin, max(max(t3[i], __float_as_int(T[i])), __float_as_int(Y[i])));
@@ -969,7 +1020,9 @@ __global__ __launch_bounds__(64) void mfma_probe_kernel(RenderParams p, const fl
 // rays leave the filter's range sweeps with the scalar-path filter instead.
 template <MfmaSpec S>
 __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves))) void render_mfma(RenderParams p) {
-    using WL = std::conditional_t<S.k16, std::conditional_t<S.lane_lds, MfmaK16LaneLds, MfmaK16Lds>, MfmaWaveLds>;
+    using WL = std::conditional_t<
+        S.k16, std::conditional_t<S.lane_lds == 2, MfmaK16PackedLds, std::conditional_t<S.lane_lds == 1, MfmaK16LaneLds, MfmaK16Lds>>,
+        MfmaWaveLds>;
     __shared__ WL wl[S.block / 64];
     WL& sh = wl[threadIdx.x >> 6];
     if constexpr (S.lds_pad > 0) {
@@ -1050,14 +1103,28 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
         bool swept;
         if constexpr (S.k16 && S.lane_lds) {
             // the path state waits in LDS (its registers are free during the sweep)
-            lane_stash(L, sh.lane, (int)lane_id());
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            swept = sweep_k16<S>(p, sh, ro, rd, best, bi, bestK, dg, upper);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const f3 lo = L.o, ld = L.d;
-            lane_unstash(L, sh.lane, (int)lane_id());
-            L.o = lo;
-            L.d = ld;
+            if constexpr (S.lane_lds == 2) {
+                lane_stash_packed(L, sh.lane, (int)lane_id());
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                swept = sweep_k16<S>(p, sh, ro, rd, best, bi, bestK, dg, upper);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const uint32_t t0 = L.t0;
+                lane_unstash_packed(L, sh.lane, (int)lane_id());
+                L.t0 = t0;
+                // ro, rd are this lane's own ray where it has one; a lane without
+                // a ray never reads its o, d again (advance leaves only TRACE or DONE)
+                L.o = ro;
+                L.d = rd;
+            } else {
+                lane_stash(L, sh.lane, (int)lane_id());
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                swept = sweep_k16<S>(p, sh, ro, rd, best, bi, bestK, dg, upper);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const f3 lo = L.o, ld = L.d;
+                lane_unstash(L, sh.lane, (int)lane_id());
+                L.o = lo;
+                L.d = ld;
+            }
         } else if constexpr (S.k16)
             swept = sweep_k16<S>(p, sh, ro, rd, best, bi, bestK, dg, upper);
         else

@@ -643,6 +643,11 @@ const Variant kVariants[] = {
     RT2_VARIANT(197, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3); x.lane_lds = true; x.serial = 3; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser3"),
     RT2_VARIANT(198, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3); x.lane_lds = true; x.serial = 4; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser4"),
     RT2_VARIANT(199, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(2); x.lane_lds = true; x.serial = 4; return x; }()>, 256, "mfma/256/k16/coop8/w2/imax/minred/ymma/t12/llds/ser4"),
+    RT2_VARIANT(202, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.lateload = true; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp/ll"),
+    RT2_VARIANT(203, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.lateload = true; x.serial = 1; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser1/cmp/ll"),
+    RT2_VARIANT(204, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.waves = 4; x.lane_lds = 2; x.afrag_lds = true; return x; }()>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/alds/llds2/ser4/cmp"),
+    RT2_VARIANT(205, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.lane_lds = 2; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds2/ser4/cmp"),
+    RT2_VARIANT(206, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.waves = 4; x.lane_lds = 2; return x; }()>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
     RT2_VARIANT(201, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3); x.lane_lds = true; x.serial = 1; x.compact = true; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser1/cmp"),
     RT2_VARIANT(166, K_MFMA, render_mfma<k16_spec(3, false, false, true)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/rsplit"),
     RT2_VARIANT(167, K_MFMA, render_mfma<k16_spec(4, true, false, true)>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/alds/rsplit"),
