@@ -11,6 +11,7 @@
   rt2_render_host_gather and rt2_gather_slabs reproduce rt2_render_host.
 """
 import ctypes as C
+import os
 
 import numpy as np
 import pytest
@@ -174,3 +175,32 @@ def test_torch_nccl_one_rank_gather(rt2mod, config_scene, torch_cuda):
         assert np.array_equal(img.cpu().numpy(), scene.render_host(u, 0, 2))
     finally:
         dist.destroy_process_group()
+
+
+def test_comm_two_ranks(rt2mod, tmp_path):
+    """The C-ABI multi-rank paths: two processes, one GPU each, an
+    RCCL communicator through rt2_comm_init — rt2_render_host_gather with
+    uneven slabs and the 8-bit sums asked for by the root only, rt2_gather_slabs
+    of device slabs (both bit-identical to rt2_render_host), and a rank-local
+    failure that both ranks report instead of blocking.  Needs two GPUs (the
+    driver's 8-GPU node); skipped on a one-GPU box."""
+    import subprocess
+    import sys
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs")
+    worker = os.path.join(os.path.dirname(__file__), "multi_rank_worker.py")
+    out, idf = str(tmp_path / "res.json"), str(tmp_path / "comm.id")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    procs = [subprocess.Popen([sys.executable, worker, str(r), "2", idf, out], env=env) for r in range(2)]
+    try:
+        rcs = [p.wait(timeout=240) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert rcs == [0, 0]
+    import json
+    res = json.load(open(out))
+    assert res == {**res, "render_host_gather": True, "render_host_gather_rgb8": True, "gather_slabs": True,
+                   "failure_agreed": True}, res
