@@ -548,6 +548,12 @@ constexpr MfmaSpec kMfmaK16 = [] {
     x.compact = true;
     return x;
 }();
+constexpr MfmaSpec kMfmaK16W4 = [] {
+    MfmaSpec x = kMfmaK16;
+    x.waves = 4;
+    x.lane_lds = 2;
+    return x;
+}();
 constexpr Bvh3Spec kBvhDefault{.block = 256, .thresh = 16, .slab = Slab::Markstein, .waves = 5, .diag = false};
 
 #ifdef RT2_EXPERIMENTS
@@ -605,6 +611,8 @@ const Variant kVariants[] = {
     RT2_VARIANT(136, K_SMEM, render_smem<kSmemDefault>, 256, "smem/256/max3f8/coop32/w6/lockstep"),  // variant 0 forced (id 0 = automatic)
     // default brute-force kernel for every scene in the matrix filter's range (DESIGN.md "The k16 sweep")
     RT2_VARIANT(200, K_MFMA, render_mfma<kMfmaK16>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"),
+    // the same at 4 waves per SIMD (path state packed into 15 LDS words): rank slabs with < 1.5 items per 3-wave lane
+    RT2_VARIANT(206, K_MFMA, render_mfma<kMfmaK16W4>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
 #ifdef RT2_EXPERIMENTS
     RT2_VARIANT(160, K_MFMA, render_mfma<k16_spec(3)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12"),
     RT2_VARIANT(161, K_MFMA, render_mfma<k16_spec(4)>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12"),
@@ -647,7 +655,6 @@ const Variant kVariants[] = {
     RT2_VARIANT(203, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.lateload = true; x.serial = 1; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser1/cmp/ll"),
     RT2_VARIANT(204, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.waves = 4; x.lane_lds = 2; x.afrag_lds = true; return x; }()>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/alds/llds2/ser4/cmp"),
     RT2_VARIANT(205, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.lane_lds = 2; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds2/ser4/cmp"),
-    RT2_VARIANT(206, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.waves = 4; x.lane_lds = 2; return x; }()>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
     RT2_VARIANT(201, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3); x.lane_lds = true; x.serial = 1; x.compact = true; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser1/cmp"),
     RT2_VARIANT(166, K_MFMA, render_mfma<k16_spec(3, false, false, true)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/rsplit"),
     RT2_VARIANT(167, K_MFMA, render_mfma<k16_spec(4, true, false, true)>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/alds/rsplit"),
@@ -733,6 +740,8 @@ constexpr int kDefaultBrute = 0;
 constexpr int kDefaultBvh = 109;
 constexpr int kLargeScene = 86;  // tiled/512/max3f4: LDS tiles above kSmemMaxTris triangles
 constexpr int kSlab = 92;        // assist12/max3f8/w6: fewer than 4 items per lane (multi-GPU slabs)
+constexpr int kMfmaSlab = 206;  // 4 waves per SIMD: more resident lanes for launches with < 1.5 items per 3-wave
+                                // lane (config B's 1/8 slab: 39.1 vs 41.4 ms; whole image 255 vs 249 ms)
 constexpr int kMfma = 200;  // mfma/.../k16/...: the matrix-core filter on v_mfma_f32_32x32x16_f16 (DESIGN.md "The k16
                             // sweep"): config B 256 vs 283 ms for the 16x16x32 form (variant 152), config C sample
                             // 2.13 vs 2.43 s, config E sample 3.9 vs 6.9 s for the scalar LDS-tiled kernel
@@ -979,6 +988,16 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
             // slabs' tails) and every scene size: config E's 1M triangles too
             // (3.9 vs 6.9 s for kLargeScene on a 480x270 sample)
             vi = kMfma;
+            // few items per lane (the 1/8 slab of config B): the 4-wave build's
+            // extra lanes shorten the last round; it packs the path state into
+            // 16-bit fields (x, y, rays per pixel) and 12 bits of bounce count
+            const Variant* W4 = find_variant(kMfmaSlab);
+            int occ3 = 0;
+            HIPCHECK(variant_occupancy(*find_variant(kMfma), &occ3, 0));
+            const double ipl3 = (double)p.n_items / ((double)s->num_cus * std::max(occ3, 1) * 256.0);
+            if (W4 && ipl3 < 1.5 && u->width <= 65535 && u->height <= 65535 && u->maxBounceCount <= 4095 &&
+                u->numRaysPerPixel <= 65535)
+                vi = kMfmaSlab;
         } else if (vi == kDefaultBrute) {
             // scenes outside the matrix filter's range (mfma_ok = 0):
             // items per resident lane decide the tail: a lane ends on a whole

@@ -101,6 +101,7 @@ def _last_variant(rt2mod, scene):
 
 
 AUTO_MFMA = "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"  # variant 200 (the k16 sweep)
+AUTO_MFMA_SLAB = "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp"  # variant 206: < 1.5 items per lane
 
 
 def test_auto_variant_large_scene(rt2mod, config_scene, torch_cuda):
@@ -113,6 +114,25 @@ def test_auto_variant_large_scene(rt2mod, config_scene, torch_cuda):
     assert _last_variant(rt2mod, scene) == AUTO_MFMA
 
 
+def test_auto_variant_packed_state_limits(rt2mod, oraclemod, config_scene, torch_cuda):
+    """Below 1.5 items per lane the launcher takes the 4-wave k16 build, whose
+    path state packs the bounce count into 12 bits; a bounce limit above 4095
+    keeps the 3-wave build — same image either way."""
+    sd, spec = config_scene("B")
+    u = rt2mod.offline_uniforms(40, 24, spec.bounces, 3, sd.num_triangles)
+    scene = rt2mod.Scene(sd, 0)
+    img = scene.render_host(u, 0, 1)
+    assert _last_variant(rt2mod, scene) == AUTO_MFMA_SLAB
+    u.maxBounceCount = 5000
+    img2 = scene.render_host(u, 0, 1)
+    assert _last_variant(rt2mod, scene) == AUTO_MFMA
+    ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(24), 0, 1)
+    assert_exact(img2, ref, "5000 bounces")
+    u.maxBounceCount = spec.bounces
+    ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(24), 0, 1)
+    assert_exact(img, ref, "packed state")
+
+
 def test_auto_variant_by_items_per_lane(rt2mod, config_scene, torch_cuda):
     """The launcher picks the matrix-core filter kernel for the full config B
     image and for its 1/2, 1/4 and 1/8 slabs (the assist
@@ -123,7 +143,7 @@ def test_auto_variant_by_items_per_lane(rt2mod, config_scene, torch_cuda):
     scene = rt2mod.Scene(sd, 0)
     full = scene.render_host(u, 0, 1)
     assert _last_variant(rt2mod, scene) == AUTO_MFMA
-    for n, want in ((2, AUTO_MFMA), (4, AUTO_MFMA), (8, AUTO_MFMA)):
+    for n, want in ((2, AUTO_MFMA), (4, AUTO_MFMA), (8, AUTO_MFMA_SLAB)):
         sh = rt2mod.shard(1, n - 1, n)
         img = scene.render_host(u, 0, 1, sh)
         assert _last_variant(rt2mod, scene) == want
@@ -303,11 +323,11 @@ def test_frame_split_identical(rt2mod, oraclemod, config_scene, torch_cuda, trav
 
 
 # brute-force kernel variants that change the schedule, not the arithmetic:
-# the product variants (0 = automatic, 86, 92, 150/152/200 = the matrix filter, 136 = the scalar path
+# the product variants (0 = automatic, 86, 92, 150/152/200/206 = the matrix filter, 136 = the scalar path
 # forced) and, in an experiment build, the A/B
 # variants (masked/plk filters, resident LDS, cooperative and team tail modes,
 # split waves, the round-1 slab kernels, occupancy hints)
-BRUTE_VARIANTS = [0, 86, 92, 150, 152, 200, 136] + ([137, 138, 139, 140, 143, 144, 145, 146] if EXPERIMENTS else []) + ([22, 24, 28, 52, 64, 65, 66, 67, 68, 70, 71, 72, 73, 74, 76, 79, 80, 84, 85, 87, 89, 95, 97, 101, 104, 106,
+BRUTE_VARIANTS = [0, 86, 92, 150, 152, 200, 206, 136] + ([137, 138, 139, 140, 143, 144, 145, 146] if EXPERIMENTS else []) + ([22, 24, 28, 52, 64, 65, 66, 67, 68, 70, 71, 72, 73, 74, 76, 79, 80, 84, 85, 87, 89, 95, 97, 101, 104, 106,
                                  90] if EXPERIMENTS else [])
 
 
