@@ -655,6 +655,11 @@ const Variant kVariants[] = {
     RT2_VARIANT(203, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.lateload = true; x.serial = 1; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser1/cmp/ll"),
     RT2_VARIANT(204, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.waves = 4; x.lane_lds = 2; x.afrag_lds = true; return x; }()>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/alds/llds2/ser4/cmp"),
     RT2_VARIANT(205, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.lane_lds = 2; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds2/ser4/cmp"),
+    RT2_VARIANT(207, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.sol = 1; return x; }()>, 256, "SOL1/k16/200/records-of-group-0"),
+    RT2_VARIANT(208, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.tshift = 10; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t10/llds/ser4/cmp"),
+    RT2_VARIANT(209, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.tshift = 8; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t8/llds/ser4/cmp"),
+    RT2_VARIANT(210, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.diag = true; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp/diag"),
+    RT2_VARIANT(211, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.diag = true; x.tshift = 8; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t8/llds/ser4/cmp/diag"),
     RT2_VARIANT(201, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3); x.lane_lds = true; x.serial = 1; x.compact = true; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser1/cmp"),
     RT2_VARIANT(166, K_MFMA, render_mfma<k16_spec(3, false, false, true)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/rsplit"),
     RT2_VARIANT(167, K_MFMA, render_mfma<k16_spec(4, true, false, true)>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/alds/rsplit"),

@@ -28,8 +28,18 @@ ap.add_argument("--traversal", default="brute", choices=["brute", "bvh"])
 ap.add_argument("--no-split", action="store_true", help="whole-pixel items for F > 1")
 ap.add_argument("--cost-order", type=int, default=-1, help="1/0: force most-expensive-first item order on/off")
 ap.add_argument("--no-check", default="", help="comma list of variants whose image is not compared (speed-of-light probes)")
+ap.add_argument("--dup", default="", help="K,T: the scene's last K triangles repeated T times (every matrix-filter "
+                                          "group identical: isolates the record-load cost from the paths)")
 a = ap.parse_args()
 sd, spec = rt2.build_config_scene(a.config)
+if a.dup:
+    k, t = (int(x) for x in a.dup.split(","))
+    tri = sd.triangles()[-k:]
+    sd2 = rt2.SceneData()
+    for m in sd.materials():
+        sd2.add_material(rt2.Material.from_buffer_copy(m.tobytes()))
+    sd2.add_triangles(np.concatenate([tri] * t))
+    sd = sd2
 W, H, R = a.width or spec.width, a.height or spec.height, a.rays or spec.rays
 u = rt2.offline_uniforms(W, H, spec.bounces, R, sd.num_triangles)
 scene = rt2.Scene(sd, 0)
