@@ -660,6 +660,9 @@ const Variant kVariants[] = {
     RT2_VARIANT(209, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.tshift = 8; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t8/llds/ser4/cmp"),
     RT2_VARIANT(210, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.diag = true; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp/diag"),
     RT2_VARIANT(211, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.diag = true; x.tshift = 8; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t8/llds/ser4/cmp/diag"),
+    RT2_VARIANT(212, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.pipe = true; x.waves = 2; return x; }()>, 256, "mfma/256/k16/coop8/w2/imax/minred/ymma/t12/llds/ser4/cmp/pipe"),
+    RT2_VARIANT(213, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.pipe = true; x.waves = 2; x.lane_lds = 0; return x; }()>, 256, "mfma/256/k16/coop8/w2/imax/minred/ymma/t12/ser4/cmp/pipe"),
+    RT2_VARIANT(214, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.pipe = true; x.diag = true; x.waves = 2; return x; }()>, 256, "mfma/256/k16/coop8/w2/imax/minred/ymma/t12/llds/ser4/cmp/pipe/diag"),
     RT2_VARIANT(201, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3); x.lane_lds = true; x.serial = 1; x.compact = true; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser1/cmp"),
     RT2_VARIANT(166, K_MFMA, render_mfma<k16_spec(3, false, false, true)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/rsplit"),
     RT2_VARIANT(167, K_MFMA, render_mfma<k16_spec(4, true, false, true)>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/alds/rsplit"),
