@@ -748,6 +748,7 @@ constexpr int kDefaultBrute = 0;
 constexpr int kDefaultBvh = 109;
 constexpr int kLargeScene = 86;  // tiled/512/max3f4: LDS tiles above kSmemMaxTris triangles
 constexpr int kSlab = 92;        // assist12/max3f8/w6: fewer than 4 items per lane (multi-GPU slabs)
+constexpr int kMfmaSlabMaxTris = 8192;
 constexpr int kMfmaSlab = 206;  // 4 waves per SIMD: more resident lanes for launches with < 1.5 items per 3-wave
                                 // lane (config B's 1/8 slab: 39.1 vs 41.4 ms; whole image 255 vs 249 ms)
 constexpr int kMfma = 200;  // mfma/.../k16/...: the matrix-core filter on v_mfma_f32_32x32x16_f16 (DESIGN.md "The k16
@@ -998,12 +999,15 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
             vi = kMfma;
             // few items per lane (the 1/8 slab of config B): the 4-wave build's
             // extra lanes shorten the last round; it packs the path state into
-            // 16-bit fields (x, y, rays per pixel) and 12 bits of bounce count
+            // 16-bit fields (x, y, rays per pixel) and 12 bits of bounce count.
+            // Only while the records stay L2-resident: at config C's 100k
+            // triangles the fourth wave costs more than its lanes gain (a
+            // 480x270x2 sample, 1.3 items per lane: 3.13 vs 2.13 s)
             const Variant* W4 = find_variant(kMfmaSlab);
             int occ3 = 0;
             HIPCHECK(variant_occupancy(*find_variant(kMfma), &occ3, 0));
             const double ipl3 = (double)p.n_items / ((double)s->num_cus * std::max(occ3, 1) * 256.0);
-            if (W4 && ipl3 < 1.5 && u->width <= 65535 && u->height <= 65535 && u->maxBounceCount <= 4095 &&
+            if (W4 && ipl3 < 1.5 && s->n_tris <= kMfmaSlabMaxTris && u->width <= 65535 && u->height <= 65535 && u->maxBounceCount <= 4095 &&
                 u->numRaysPerPixel <= 65535)
                 vi = kMfmaSlab;
         } else if (vi == kDefaultBrute) {

@@ -106,13 +106,14 @@ AUTO_MFMA_SLAB = "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp"  # 
 
 def test_auto_variant_large_scene(rt2mod, config_scene, torch_cuda):
     """Scenes whose matrix-filter records outgrow an XCD's L2 (config C: 100k
-    triangles, 22 MB of k16 records) run the same k16 matrix kernels (this
-    small image has < 1.5 items per lane: the 4-wave build)."""
+    triangles, 22 MB of k16 records) run the same k16 matrix kernel, and the
+    3-wave build even below 1.5 items per lane (this small image): the 4-wave
+    build serves only scenes of <= 8,192 triangles."""
     sd, spec = config_scene("C")
     u = rt2mod.offline_uniforms(64, 36, spec.bounces, 1, sd.num_triangles)
     scene = rt2mod.Scene(sd, 0)
     scene.render_host(u, 0, 1)
-    assert _last_variant(rt2mod, scene) == AUTO_MFMA_SLAB
+    assert _last_variant(rt2mod, scene) == AUTO_MFMA
 
 
 def test_auto_variant_packed_state_limits(rt2mod, oraclemod, config_scene, torch_cuda):
