@@ -68,7 +68,9 @@ struct MfmaSpec {
                             // interleaved with the previous block's reduction, the exact phase trails by one group
     int tile_groups = 0;    // k16 (render_mfma_tiled): 32-triangle groups per LDS record tile shared by the workgroup
     int sol = 0;            // speed-of-light probes (WRONG images; diag clocks only): 1 = every group reads group
-                            // 0's records, 2 = no exact phase, 3 = 2 + only the U term is reduced
+                            // 0's records, 2 = no exact phase, 3 = 2 + only the U term is reduced; marginal-cost
+                            // probes (same image): 4 = exact phase twice, 5 = products and reduction twice,
+                            // 6 = the reduction's VALU twice, 7 = the products twice
 };
 
 // per-wave diagnostic counts of sweep_mfma (wave-uniform; MfmaSpec::diag)
@@ -654,6 +656,9 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, SH& sh, const f
         if constexpr (S.afrag_lds) read_a();
         const float Tl = tau * sc.Tw;
         int tmin = 0x7fffffff;
+        [[maybe_unused]] int u3[16], tmin6 = 0;
+        [[maybe_unused]] f16v ex = {};
+        if constexpr (S.sol == 7) ex[0] = p.mfma_A * 0.0f;
 #pragma unroll
         for (int R = 0; R < 2; R++) {
             if (R == 1 && !upper) break;
@@ -670,9 +675,21 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, SH& sh, const f
 #pragma unroll
                 for (int i = 0; i < 16; i++)
                     t3[i] = max(max(__float_as_int(U[i]), __float_as_int(V[i])), __float_as_int(X[i]));
+                if constexpr (S.sol == 6) {
+                    // marginal-cost probe: the reduction's VALU once more (min/max swapped: no CSE)
+#pragma unroll
+                    for (int i = 0; i < 16; i++)
+                        u3[i] = min(min(__float_as_int(U[i]), __float_as_int(V[i])), __float_as_int(X[i]));
+                }
                 __builtin_amdgcn_sched_barrier(0);
                 const f16v T = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[R], b[6], zero, 0, 0, 0);
                 const f16v Y = __builtin_amdgcn_mfma_f32_32x32x16_f16(y1[R], b[6], zero, 0, 0, 0);
+                if constexpr (S.sol == 7) {
+                    // marginal-cost probe: the block's 8 products once more, one chain (sunk per group)
+#pragma unroll
+                    for (int k = 0; k < 8; k++)
+                        ex = __builtin_amdgcn_mfma_f32_32x32x16_f16(k < 3 ? a0[R] : a1[R], b[k < 7 ? k : 6], ex, 0, 0, 0);
+                }
                 __builtin_amdgcn_sched_barrier(0);
                 if constexpr (S.lateload) {
                     // the group's last product is issued: its operand registers
@@ -686,6 +703,11 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, SH& sh, const f
 #pragma unroll
                 for (int i = 0; i < 16; i++)
                     tmin = min(tmin, max(max(t3[i], __float_as_int(T[i])), __float_as_int(Y[i])));
+                if constexpr (S.sol == 6) {
+#pragma unroll
+                    for (int i = 0; i < 16; i++)
+                        tmin6 = max(tmin6, min(min(u3[i], __float_as_int(T[i])), __float_as_int(Y[i])));
+                }
                 // serial 3: block R's last reduction may overlap block R+1's products;
                 // serial 4: and the next group's record loads may move up
                 if constexpr (S.serial == 1) __builtin_amdgcn_sched_barrier(0);
@@ -739,6 +761,10 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, SH& sh, const f
             }
             if (tmin2 == 0x12345677) best = -best;  // never (a sink)
         }
+        if constexpr (S.sol == 6)
+            if (tmin6 == 0x12345677) best = -best;  // never (a sink)
+        if constexpr (S.sol == 7)
+            if (ex[0] == 1.2345e-30f) best = -best;  // never (a sink)
         const unsigned long long M = (S.sol == 2 || S.sol == 3) ? (unsigned long long)(tmin == 0x7ffffffe)
                                                                  : __ballot(tmin <= __float_as_int(Tl));
         if constexpr (S.diag) dg.groups += 1;

@@ -663,6 +663,10 @@ const Variant kVariants[] = {
     RT2_VARIANT(212, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.pipe = true; x.waves = 2; return x; }()>, 256, "mfma/256/k16/coop8/w2/imax/minred/ymma/t12/llds/ser4/cmp/pipe"),
     RT2_VARIANT(213, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.pipe = true; x.waves = 2; x.lane_lds = 0; return x; }()>, 256, "mfma/256/k16/coop8/w2/imax/minred/ymma/t12/ser4/cmp/pipe"),
     RT2_VARIANT(214, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.pipe = true; x.diag = true; x.waves = 2; return x; }()>, 256, "mfma/256/k16/coop8/w2/imax/minred/ymma/t12/llds/ser4/cmp/pipe/diag"),
+    RT2_VARIANT(218, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.sol = 6; return x; }()>, 256, "SOL6/k16/200/reduction-VALU-twice"),
+    RT2_VARIANT(219, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.sol = 7; return x; }()>, 256, "SOL7/k16/200/products-twice"),
+    RT2_VARIANT(220, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.sol = 5; return x; }()>, 256, "SOL5/k16/200/products-and-reduction-twice"),
+    RT2_VARIANT(221, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.sol = 4; return x; }()>, 256, "SOL4/k16/200/exact-phase-twice"),
     RT2_VARIANT(201, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3); x.lane_lds = true; x.serial = 1; x.compact = true; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser1/cmp"),
     RT2_VARIANT(166, K_MFMA, render_mfma<k16_spec(3, false, false, true)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/rsplit"),
     RT2_VARIANT(167, K_MFMA, render_mfma<k16_spec(4, true, false, true)>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/alds/rsplit"),
