@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -1032,6 +1033,17 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
         VP = find_variant(vi);
     }
     const Variant& V = *VP;
+    // XCD-group item regions serve the BVH walk's L2 locality; the brute-force
+    // kernels read the same records for every ray, so they take items from one
+    // counter in dispatch order, which spreads neighbouring 64-pixel runs over
+    // the XCDs (with <= 1 item per lane a region is one XCD's whole share: an
+    // expensive band of rows would set the launch's end).  RT2_ITEM_REGIONS=0/1
+    // forces the choice (A/B runs).
+    static const int regions_env = [] {
+        const char* e = std::getenv("RT2_ITEM_REGIONS");
+        return e && *e ? std::atoi(e) : -1;
+    }();
+    if (regions_env == 0 || (regions_env < 0 && !is_bvh(V.kind))) p.region_ctr = nullptr;
     size_t lds = 0;
     if (V.kind == K_TILED)
         lds = (size_t)3 * sizeof(float4) * kTileTris;
