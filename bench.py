@@ -59,6 +59,7 @@ L2_PEAK_GBS = 34500.0      # MI355X_MICROARCH.md §L2: ≈34.5 TB/s aggregate
 MFMA_F16_PEAK_TFLOPS = 2500.0  # MI355X dense F16/BF16 matrix peak (MI355X_MICROARCH.md; no sparsity)
 MFMA_FLOP_PER_PAIR = 320   # render_mfma 16x16x32 form: 5 quantities x 32 k-slots x 2 per (ray, triangle) pair
 MFMA_K16_FLOP_PER_PAIR = 256  # the k16 sweep: 8 v_mfma_f32_32x32x16_f16 (32x32x16x2 FLOP each) per 1,024 pairs
+MFMA_K5_FLOP_PER_PAIR = 160   # its 5-product form (MfmaSpec::k5): 5 v_mfma_f32_32x32x16_f16 per 1,024 pairs
 TARGET_RATIO = 10.0        # north star: >= 10x the CPU reference at config C on 1 GPU
 KERNEL_FILES = {"mfma": "render_mfma", "massist": "render_assist", "smem": "render_smem", "split": "render_split", "tiled": "render_tiled", "assist": "render_assist",
                 "resident": "render_resident", "bvh4": "render_bvh4", "bvh3": "render_bvh3", "bvh2": "render_bvh2",
@@ -205,12 +206,15 @@ def roofline(tests, visits, kern_ms, segments=0, n_tris=0, variant=None):
                                    "frac": round(hbm / HBM_PEAK_GBS, 3),
                                    "note": "36 B x tests; >1 = on-chip reuse (effective bandwidth)"}}
     if variant and variant.startswith(("mfma", "massist")) and segments and n_tris:
-        k16 = "/k16/" in variant
+        k5 = "/k5/" in variant
+        k16 = "/k16/" in variant or k5
         group = 32 if k16 else 16
         pairs = segments * (-(-int(n_tris) // group) * group)
-        fpp = MFMA_K16_FLOP_PER_PAIR if k16 else MFMA_FLOP_PER_PAIR
+        fpp = MFMA_K5_FLOP_PER_PAIR if k5 else MFMA_K16_FLOP_PER_PAIR if k16 else MFMA_FLOP_PER_PAIR
         mf = fpp * pairs / (kern_ms * 1e-3) / 1e12
-        model = ("256 x (ray, triangle) pairs: the k16 sweep's 8 v_mfma_f32_32x32x16_f16 per 32 rays x 32 "
+        model = ("160 x (ray, triangle) pairs: the 5-product k16 form's 5 v_mfma_f32_32x32x16_f16 per 32 rays x 32 "
+                 "triangles (U, -V, X, -tn, Y: one K-half each), triangles padded to 32" if k5 else
+                 "256 x (ray, triangle) pairs: the k16 sweep's 8 v_mfma_f32_32x32x16_f16 per 32 rays x 32 "
                  "triangles (U, -V, X: two K-halves each; -tn, Y: one), triangles padded to 32"
                  if k16 else "320 x (ray, triangle) pairs (5 f16x3 products of 32 k-slots per pair, triangles "
                              "padded to 16)")

@@ -61,6 +61,8 @@ struct MfmaSpec {
     bool lateload = false;  // k16 (serial 1/3/4): the next group's records are requested into the operand registers
                             // right after this group's last product is issued (no extra VGPRs)
     bool compact = false;   // k16: <= 32 live rays move to lanes 0..31 and the second 32-ray block is skipped
+    bool k5 = false;        // k16: U, -V, X from the first K-half only (5 products per 32-ray block instead of 8);
+                            // the two m.z slots left out are bounded per (wave, triangle) and added to the threshold
     int serial = 0;         // k16: scheduling fences per 32-ray block: 1 = U V X products | their max | -tn Y
                             // products | the rest (48 accumulator VGPRs live); 2 = all 8 products | the reduction;
                             // 3 = 1 without the fence between the blocks; 4 = 3 without the fence at the group end
@@ -545,20 +547,31 @@ __device__ __forceinline__ void lane_unstash(Lane& L, const uint32_t (*st)[64], 
     L.t0 = st[19][l];
 }
 
-__global__ void prep_mfma_k16(const float4* tri, int n, int n_pad, _Float16* out, float* tau_out, uint32_t* flags) {
+// bnd_out (the 5-product form, MfmaSpec::k5): per triangle, the largest
+// |slot 16| and |slot 17| over U, -V, X — the m.z products hi x ray-lo and
+// lo x ray-hi that the form leaves out (sweep_k16 adds their bound to the
+// threshold)
+__global__ void prep_mfma_k16(const float4* tri, int n, int n_pad, _Float16* out, float* tau_out, float2* bnd_out,
+                              uint32_t* flags) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_pad) return;
     MfmaCoef k;
     mfma_coefs(tri, i, n, k, flags);
     const int G = i >> 5, t = i & 31;
+    float ch = 0.0f, cl = 0.0f;
     for (int op = 0; op < kK16Ops; op++) {
         const int q = op < 6 ? op >> 1 : 3, h = op < 6 ? (op & 1) : 1;
         _Float16 slot[32];
         mfma_slots(k.c[q], k.tau, slot);
         for (int j = 0; j < 16; j++)
             out[((size_t)(G * kK16Ops + op) * 64 + t + 32 * (j >> 3)) * 8 + (j & 7)] = slot[16 * h + j];
+        if (op < 6) {
+            ch = fmaxf(ch, fabsf((float)slot[16]));
+            cl = fmaxf(cl, fabsf((float)slot[17]));
+        }
     }
     tau_out[i] = (float)k.tau;
+    if (bnd_out) bnd_out[i] = make_float2(ch, cl);
 }
 
 // The five terms of 32 rays (fragments a0/a1 = the main fragment's two
@@ -591,12 +604,26 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, SH& sh, const f
     static_assert(S.ymma && S.imax && S.minred, "the k16 sweep implements the ymma / imax / minred form");
     if constexpr (S.pipe)
         if (upper) return sweep_k16_pipe<S>(p, sh, o, d, best, bi, bestK, dg);
+    static_assert(!S.k5 || (!S.prefetch && !S.lateload && !S.afrag_lds && (S.serial == 1 || S.serial == 3 || S.serial == 4)),
+                  "the 5-product form is built on the serialised sweep");
     const int lane = (int)lane_id();
     const int r32 = lane & 31, hl = lane >> 5;
     const f3 m = cross(d, o);
     MfmaScale sc;
     if (!mfma_scale<S>(p.mfma_A, o, d, m, sc)) return false;
     mfma_main_row(&sh.ray[lane][0], d, m, o, sc.sigma);
+    // k5: the wave's largest |ray lo| and |ray hi| of m.z (slots 16 and 17 of
+    // the main fragment, the same arithmetic as mfma_main_row): with the
+    // records' per-triangle |hi|, |lo| of the m.z coefficients they bound the
+    // two products the 5-product form leaves out of U, -V and X
+    [[maybe_unused]] float zlo = 0.0f, zhi = 0.0f;
+    if constexpr (S.k5) {
+        const float vz = m.z * sc.sigma;
+        const _Float16 hz = (_Float16)vz;
+        const _Float16 lz = (_Float16)(vz - (float)hz);
+        zhi = wave_max(fabsf((float)hz));
+        zlo = wave_max(fabsf((float)lz));
+    }
     auto write_y = [&](float bkv) {
         _Float16 s[16];
         mfma_y_chunk(s, d, o, bkv, sc.sigma, sc.Bmax);
@@ -628,10 +655,17 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, SH& sh, const f
     const float* tg = p.mfma_k16_tau + r32;
     h8 b[kK16Ops], nb[kK16Ops];
     float tau = 0.0f, ntau = 0.0f;
+    [[maybe_unused]] float2 bnd = make_float2(0.0f, 0.0f);
+    [[maybe_unused]] const float2* bg = p.mfma_k16_bnd + r32;
     auto fetch = [&](h8* dst, float& t) {
 #pragma unroll
-        for (int op = 0; op < kK16Ops; op++) dst[op] = fg[64 * op];
+        for (int op = 0; op < kK16Ops; op++)
+            if (!S.k5 || !(op & 1) || op == 6) dst[op] = fg[64 * op];  // k5: the second K-halves of U V X unused
         t = *tg;
+        if constexpr (S.k5) {
+            bnd = *bg;
+            bg += 32;
+        }
         fg += kK16Ops * 64;
         tg += 32;
     };
@@ -654,7 +688,11 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, SH& sh, const f
             fetch(b, tau);
         }
         if constexpr (S.afrag_lds) read_a();
-        const float Tl = tau * sc.Tw;
+        float Tl = tau * sc.Tw;
+        // k5: + |c_hi| max|ray lo| + |c_lo| max|ray hi| of the left-out m.z
+        // slots, padded by 2^-10 for its own rounding ("The
+        // 5-product form")
+        if constexpr (S.k5) Tl += (bnd.x * zlo + bnd.y * zhi) * 1.0009765625f;
         int tmin = 0x7fffffff;
         [[maybe_unused]] int u3[16], tmin6 = 0;
         [[maybe_unused]] f16v ex = {};
@@ -667,9 +705,11 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, SH& sh, const f
                 f16v U = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[R], b[0], zero, 0, 0, 0);
                 f16v V = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[R], b[2], zero, 0, 0, 0);
                 f16v X = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[R], b[4], zero, 0, 0, 0);
-                U = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[R], b[1], U, 0, 0, 0);
-                V = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[R], b[3], V, 0, 0, 0);
-                X = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[R], b[5], X, 0, 0, 0);
+                if constexpr (!S.k5) {
+                    U = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[R], b[1], U, 0, 0, 0);
+                    V = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[R], b[3], V, 0, 0, 0);
+                    X = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[R], b[5], X, 0, 0, 0);
+                }
                 __builtin_amdgcn_sched_barrier(0);
                 int t3[16];
 #pragma unroll
@@ -834,12 +874,26 @@ template <MfmaSpec S, class SH>
 __device__ __forceinline__ bool sweep_k16_pipe(const RenderParams& p, SH& sh, const f3& o, const f3& d, float& best,
                                                int& bi, float& bestK, MfmaDiag& dg) {
     static_assert(S.k16 && S.ymma && S.imax && S.minred, "the pipelined k16 sweep implements the k16 ymma / minred form");
+    static_assert(!S.k5 || (!S.prefetch && !S.lateload && !S.afrag_lds && (S.serial == 1 || S.serial == 3 || S.serial == 4)),
+                  "the 5-product form is built on the serialised sweep");
     const int lane = (int)lane_id();
     const int r32 = lane & 31, hl = lane >> 5;
     const f3 m = cross(d, o);
     MfmaScale sc;
     if (!mfma_scale<S>(p.mfma_A, o, d, m, sc)) return false;
     mfma_main_row(&sh.ray[lane][0], d, m, o, sc.sigma);
+    // k5: the wave's largest |ray lo| and |ray hi| of m.z (slots 16 and 17 of
+    // the main fragment, the same arithmetic as mfma_main_row): with the
+    // records' per-triangle |hi|, |lo| of the m.z coefficients they bound the
+    // two products the 5-product form leaves out of U, -V and X
+    [[maybe_unused]] float zlo = 0.0f, zhi = 0.0f;
+    if constexpr (S.k5) {
+        const float vz = m.z * sc.sigma;
+        const _Float16 hz = (_Float16)vz;
+        const _Float16 lz = (_Float16)(vz - (float)hz);
+        zhi = wave_max(fabsf((float)hz));
+        zlo = wave_max(fabsf((float)lz));
+    }
     auto write_y = [&](float bkv) {
         _Float16 s[16];
         mfma_y_chunk(s, d, o, bkv, sc.sigma, sc.Bmax);
@@ -1184,7 +1238,14 @@ __global__ __launch_bounds__(64) void mfma_probe_kernel(RenderParams p, const fl
                 const h8 a0 = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][8 * hl]);
                 const h8 a1 = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][16 + 8 * hl]);
                 const h8 y1 = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][32 + 8 * hl]);
-                const K16Terms q = k16_terms(a0, a1, y1, b);
+                K16Terms q = k16_terms(a0, a1, y1, b);
+                if constexpr (S.k5) {
+                    // the 5-product form: U, -V, X from the first K-half only
+                    const f16v zero = {};
+                    q.U = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b[0], zero, 0, 0, 0);
+                    q.V = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b[2], zero, 0, 0, 0);
+                    q.X = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b[4], zero, 0, 0, 0);
+                }
                 for (int i = 0; i < 16; i++) {
                     const size_t rr = ray0 + 32 * R + 8 * (i >> 2) + 4 * hl + (i & 3);
                     float* tt = terms + (rr * n_pad + 32 * G + r32) * 5;
@@ -1247,6 +1308,17 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
     MfmaDiag dg;
     unsigned long long tc = 0;  // diag: s_memtime at the current phase's start
     if constexpr (S.diag) tc = __builtin_amdgcn_s_memtime();
+    // diag wave timeline (p.wave_log, 10 words per wave): start, first lane out
+    // of items, end (s_memrealtime, 100 MHz), segment rounds with two 32-ray
+    // blocks, with one, idle (lockstep: the wave had no ray), cooperative drain,
+    // the wave's place (HW_ID | XCC_ID << 32), and shader clocks (s_memtime) at
+    // start and end: their ratio to the real-time ticks is the in-kernel clock
+    unsigned long long wl_t0 = 0, wl_c0 = 0, wl_dry = 0, wl_r2 = 0, wl_r1 = 0, wl_idle = 0, wl_coop = 0;
+    if constexpr (S.diag)
+        if (p.wave_log) {
+            wl_t0 = __builtin_amdgcn_s_memrealtime();
+            wl_c0 = __builtin_amdgcn_s_memtime();
+        }
     auto stamp = [&](unsigned long long& acc) {
         if constexpr (S.diag) {
             const unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -1258,11 +1330,24 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
         advance(L, p);
         unsigned long long act = __ballot(L.st == ST_TRACE);
         stamp(dg.t_advance);
+        if constexpr (S.diag)
+            if (p.wave_log && !wl_dry && __any(L.st == ST_DONE)) wl_dry = __builtin_amdgcn_s_memrealtime();
         if constexpr (S.lockstep) {
             if (!__syncthreads_or(act != 0)) break;
-            if (!act) continue;
+            if (!act) {
+                if constexpr (S.diag) wl_idle++;
+                continue;
+            }
         } else if (!act) {
             break;
+        }
+        if constexpr (S.diag) {
+            if (__popcll(act) <= (unsigned)S.tail_lanes && __any(L.st == ST_DONE))
+                wl_coop++;
+            else if (S.compact && __popcll(act) <= 32)
+                wl_r1++;
+            else
+                wl_r2++;
         }
         if (__popcll(act) <= (unsigned)S.tail_lanes && __any(L.st == ST_DONE)) {
             float mybest = 1e38f;
@@ -1353,6 +1438,26 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
         stamp(dg.t_shade);
     }
     flush_counters(L, p);
+    if constexpr (S.diag)
+        if (p.wave_log) {
+            const uint32_t gw = blockIdx.x * (S.block / 64) + (threadIdx.x >> 6);
+            const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+            const unsigned long long hw = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+                                          (unsigned long long)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32;
+            if (lane_id() == 0 && gw < p.wave_log_n) {
+                unsigned long long* e = p.wave_log + 10 * (size_t)gw;
+                e[0] = wl_t0;
+                e[1] = wl_dry;
+                e[2] = __builtin_amdgcn_s_memrealtime();
+                e[3] = wl_r2;
+                e[4] = wl_r1;
+                e[5] = wl_idle;
+                e[6] = wl_coop;
+                e[7] = hw;
+                e[8] = wl_c0;
+                e[9] = c1;
+            }
+        }
     if constexpr (S.diag)
         if (lane_id() == 0) {
             atomicAdd(p.seg_counter + 1, dg.groups);  // (wave, triangle group) sweeps

@@ -79,6 +79,7 @@ struct rt2_scene {
     float* d_mfma_tau = nullptr;                // per-triangle record scale
     _Float16* d_mfma_k16 = nullptr;             // sweep_k16 records (32-triangle groups, 7 KiB each)
     float* d_mfma_k16_tau = nullptr;            // per-triangle record scale (same values as d_mfma_tau)
+    float2* d_mfma_k16_bnd = nullptr;           // per-triangle m.z residual bounds of the 5-product form (k5)
     int mfma_ok = 0;                            // render_mfma usable (records built, scene in range)
     float mfma_A = 0.0f;                        // max |a_i| over the in-range triangles
     float4* d_fb = nullptr;                     // frame_split scratch (per-frame colours)
@@ -429,8 +430,9 @@ static int scene_init(rt2_scene* s, const rt2_triangle* tris, int32_t n_tris, co
         const int n_pad32 = (n_tris + 31) / 32 * 32;
         HIPCHECK(hipMalloc(&s->d_mfma_k16, (size_t)n_pad32 * kK16Ops * 16 * sizeof(_Float16)));
         HIPCHECK(hipMalloc(&s->d_mfma_k16_tau, (size_t)n_pad32 * sizeof(float)));
+        HIPCHECK(hipMalloc(&s->d_mfma_k16_bnd, (size_t)n_pad32 * sizeof(float2)));
         hipLaunchKernelGGL(prep_mfma_k16, dim3((n_pad32 + 255) / 256), dim3(256), 0, 0, s->d_tri, n_tris, n_pad32,
-                           s->d_mfma_k16, s->d_mfma_k16_tau, d_mflags);
+                           s->d_mfma_k16, s->d_mfma_k16_tau, s->d_mfma_k16_bnd, d_mflags);
         HIPCHECK(hipGetLastError());
         HIPCHECK(hipMemset(d_mflags, 0, 2 * sizeof(uint32_t)));
     }
@@ -452,6 +454,7 @@ extern "C" void rt2_scene_destroy(rt2_scene* s) {
     (void)hipFree(s->d_mfma_tau);
     (void)hipFree(s->d_mfma_k16);
     (void)hipFree(s->d_mfma_k16_tau);
+    (void)hipFree(s->d_mfma_k16_bnd);
     (void)hipFree(s->d_fb);
     (void)hipFree(s->d_cost);
     (void)hipFree(s->d_order);
@@ -555,6 +558,16 @@ constexpr MfmaSpec kMfmaK16W4 = [] {
     x.lane_lds = 2;
     return x;
 }();
+constexpr MfmaSpec kMfmaK5 = [] {
+    MfmaSpec x = kMfmaK16;
+    x.k5 = true;
+    return x;
+}();
+constexpr MfmaSpec kMfmaK5W4 = [] {
+    MfmaSpec x = kMfmaK16W4;
+    x.k5 = true;
+    return x;
+}();
 constexpr Bvh3Spec kBvhDefault{.block = 256, .thresh = 16, .slab = Slab::Markstein, .waves = 5, .diag = false};
 
 #ifdef RT2_EXPERIMENTS
@@ -614,6 +627,10 @@ const Variant kVariants[] = {
     RT2_VARIANT(200, K_MFMA, render_mfma<kMfmaK16>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"),
     // the same at 4 waves per SIMD (path state packed into 15 LDS words): rank slabs with < 1.5 items per 3-wave lane
     RT2_VARIANT(206, K_MFMA, render_mfma<kMfmaK16W4>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
+    // default brute-force kernel (DESIGN.md "The 5-product form"): the k16 sweep with U, -V, X from the first K-half,
+    // the left-out m.z slots bounded in the threshold; 3 waves per SIMD, and 4 for launches with < 1.5 items per lane
+    RT2_VARIANT(227, K_MFMA, render_mfma<kMfmaK5>, 256, "mfma/256/k5/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"),
+    RT2_VARIANT(228, K_MFMA, render_mfma<kMfmaK5W4>, 256, "mfma/256/k5/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
 #ifdef RT2_EXPERIMENTS
     RT2_VARIANT(160, K_MFMA, render_mfma<k16_spec(3)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12"),
     RT2_VARIANT(161, K_MFMA, render_mfma<k16_spec(4)>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12"),
@@ -664,6 +681,15 @@ const Variant kVariants[] = {
     RT2_VARIANT(212, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.pipe = true; x.waves = 2; return x; }()>, 256, "mfma/256/k16/coop8/w2/imax/minred/ymma/t12/llds/ser4/cmp/pipe"),
     RT2_VARIANT(213, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.pipe = true; x.waves = 2; x.lane_lds = 0; return x; }()>, 256, "mfma/256/k16/coop8/w2/imax/minred/ymma/t12/ser4/cmp/pipe"),
     RT2_VARIANT(214, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.pipe = true; x.diag = true; x.waves = 2; return x; }()>, 256, "mfma/256/k16/coop8/w2/imax/minred/ymma/t12/llds/ser4/cmp/pipe/diag"),
+    RT2_VARIANT(222, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16W4; x.diag = true; return x; }()>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp/diag"),
+    // the 5-product form (MfmaSpec::k5): U, -V, X from the first K-half, the m.z residual bounded in the threshold
+    RT2_VARIANT(229, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.k5 = true; x.diag = true; return x; }()>, 256, "mfma/256/k5/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp/diag"),
+    RT2_VARIANT(230, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.k5 = true; x.waves = 4; return x; }()>, 256, "mfma/256/k5/coop8/w4/imax/minred/ymma/t12/llds/ser4/cmp"),
+    // the k16 kernels without the workgroup's per-segment barrier (waves run free)
+    RT2_VARIANT(223, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.lockstep = false; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp/free"),
+    RT2_VARIANT(224, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16W4; x.lockstep = false; return x; }()>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp/free"),
+    RT2_VARIANT(225, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.lockstep = false; x.diag = true; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp/free/diag"),
+    RT2_VARIANT(226, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16W4; x.lockstep = false; x.diag = true; return x; }()>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp/free/diag"),
     RT2_VARIANT(218, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.sol = 6; return x; }()>, 256, "SOL6/k16/200/reduction-VALU-twice"),
     RT2_VARIANT(219, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.sol = 7; return x; }()>, 256, "SOL7/k16/200/products-twice"),
     RT2_VARIANT(220, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.sol = 5; return x; }()>, 256, "SOL5/k16/200/products-and-reduction-twice"),
@@ -754,11 +780,11 @@ constexpr int kDefaultBvh = 109;
 constexpr int kLargeScene = 86;  // tiled/512/max3f4: LDS tiles above kSmemMaxTris triangles
 constexpr int kSlab = 92;        // assist12/max3f8/w6: fewer than 4 items per lane (multi-GPU slabs)
 constexpr int kMfmaSlabMaxTris = 8192;
-constexpr int kMfmaSlab = 206;  // 4 waves per SIMD: more resident lanes for launches with < 1.5 items per 3-wave
-                                // lane (config B's 1/8 slab: 39.1 vs 41.4 ms; whole image 255 vs 249 ms)
-constexpr int kMfma = 200;  // mfma/.../k16/...: the matrix-core filter on v_mfma_f32_32x32x16_f16 (DESIGN.md "The k16
-                            // sweep"): config B 256 vs 283 ms for the 16x16x32 form (variant 152), config C sample
-                            // 2.13 vs 2.43 s, config E sample 3.9 vs 6.9 s for the scalar LDS-tiled kernel
+constexpr int kMfmaSlab = 228;  // 4 waves per SIMD: more resident lanes for launches with < 1.5 items per 3-wave
+                                // lane (config B's 1/8 slab: 32.1 vs 38.6 ms for variant 227; k16: 39.1 vs 41.4 ms)
+constexpr int kMfma = 227;  // mfma/.../k5/...: the matrix-core filter on v_mfma_f32_32x32x16_f16, 5 products per
+                            // 32-ray block (DESIGN.md "The 5-product form"): config B 214 vs 261 ms for the 8-product
+                            // k16 sweep (variant 200), config C sample 1.85 vs 2.08 s, config E sample 2.42 vs 2.63 s
 
 constexpr bool is_bvh(int kind) { return kind >= K_BVH && kind <= K_BVH4; }
 
@@ -851,6 +877,7 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     p.mfma_A = s->mfma_A;
     p.mfma_k16_frag = s->d_mfma_k16;
     p.mfma_k16_tau = s->d_mfma_k16_tau;
+    p.mfma_k16_bnd = s->d_mfma_k16_bnd;
     p.tri_mtl = s->d_mtl;
     p.raw = s->d_raw;
     p.texels = s->d_texels;
@@ -1285,7 +1312,7 @@ extern "C" int rt2_device_selftest(const float* in, int32_t n, float* out10) {
 // Not in rt2.h (test hook): copies one of the scene's derived device arrays to
 // host memory: 0 = pre-transformed triangles (3 float4 each), 1 = render_mfma
 // records (16x16x32 layout), 2 = their per-triangle tau, 3 = sweep_k16 records,
-// 4 = their tau.  Returns the array's size in bytes (nothing copied when
+// 4 = their tau, 5 = the k5 form's per-triangle m.z residual bounds.  Returns the array's size in bytes (nothing copied when
 // `host` is null or `bytes` is too small), < 0 on error.
 extern "C" long long rt2_scene_export(rt2_scene* s, int what, void* host, unsigned long long bytes) {
     if (!s) return -1;
@@ -1299,6 +1326,7 @@ extern "C" long long rt2_scene_export(rt2_scene* s, int what, void* host, unsign
     case 2: src = s->d_mfma_tau, sz = n16 * sizeof(float); break;
     case 3: src = s->d_mfma_k16, sz = n32 * kK16Ops * 16 * sizeof(_Float16); break;
     case 4: src = s->d_mfma_k16_tau, sz = n32 * sizeof(float); break;
+    case 5: src = s->d_mfma_k16_bnd, sz = n32 * sizeof(float2); break;
     default: return -1;
     }
     if (!src || s->n_tris == 0) return 0;
@@ -1314,19 +1342,20 @@ extern "C" long long rt2_scene_export(rt2_scene* s, int what, void* host, unsign
 // (mfma_probe_kernel) for n_rays rays (a multiple of 64; 8 floats each: o.xyz,
 // best, d.xyz, 0) against every triangle of the scene.  layout 0 = the
 // 16x16x32 form of render_mfma (variants 150/152), 1 = the k16 form
-// (sweep_k16).  Host outputs, sized by the caller: terms [n_rays][n_pad][5]
+// (sweep_k16), 2 = its 5-product form (MfmaSpec::k5: U, -V, X from the first
+// K-half).  Host outputs, sized by the caller: terms [n_rays][n_pad][5]
 // (n_pad = triangles padded to 16 / 32), frags [n_rays][48] f16 bits, rinfo
 // [n_rays][8], accept [n_rays][n_tris].
 extern "C" int rt2_mfma_probe(rt2_scene* s, int layout, const float* rays, int32_t n_rays, float* terms,
                               uint16_t* frags, float* rinfo, uint8_t* accept) {
     if (!s || !rays || n_rays <= 0 || n_rays % 64 != 0 || !terms || !frags || !rinfo || !accept ||
-        (layout != 0 && layout != 1) || s->n_tris < 1 || !s->mfma_ok) {
+        layout < 0 || layout > 2 || s->n_tris < 1 || !s->mfma_ok) {
         rt2h::set_error("rt2_mfma_probe: bad argument (n_rays a positive multiple of 64, a scene in the filter's "
                         "range)");
         return -1;
     }
     HIPCHECK(hipSetDevice(s->device));
-    const int n_pad = layout == 1 ? (s->n_tris + 31) / 32 * 32 : (s->n_tris + 15) / 16 * 16;
+    const int n_pad = layout >= 1 ? (s->n_tris + 31) / 32 * 32 : (s->n_tris + 15) / 16 * 16;
     const size_t nr = (size_t)n_rays;
     const size_t b_rays = nr * 8 * sizeof(float), b_terms = nr * n_pad * 5 * sizeof(float),
                  b_frags = nr * 48 * sizeof(uint16_t), b_info = nr * 8 * sizeof(float), b_acc = nr * s->n_tris;
@@ -1351,9 +1380,18 @@ extern "C" int rt2_mfma_probe(rt2_scene* s, int layout, const float* rays, int32
         p.mfma_A = s->mfma_A;
         p.mfma_k16_frag = s->d_mfma_k16;
         p.mfma_k16_tau = s->d_mfma_k16_tau;
+        p.mfma_k16_bnd = s->d_mfma_k16_bnd;
         constexpr MfmaSpec k16 = k16_spec(3), f16x32 = kMfmaT8Y4;
+        constexpr MfmaSpec k5 = [] {
+            MfmaSpec x = k16_spec(3);
+            x.k5 = true;
+            return x;
+        }();
         if (layout == 1)
             hipLaunchKernelGGL(mfma_probe_kernel<k16>, dim3(n_rays / 64), dim3(64), 0, 0, p, d_rays, n_pad, d_terms,
+                               d_frags, d_info, d_acc);
+        else if (layout == 2)
+            hipLaunchKernelGGL(mfma_probe_kernel<k5>, dim3(n_rays / 64), dim3(64), 0, 0, p, d_rays, n_pad, d_terms,
                                d_frags, d_info, d_acc);
         else
             hipLaunchKernelGGL(mfma_probe_kernel<f16x32>, dim3(n_rays / 64), dim3(64), 0, 0, p, d_rays, n_pad,

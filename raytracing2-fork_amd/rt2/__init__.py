@@ -583,7 +583,8 @@ class Scene:
 
     def export(self, what: int, dtype) -> np.ndarray:
         """A derived device array of the scene (rt2_scene_export, test hook): 0 =
-        pre-transformed triangles, 1/2 = render_mfma records/tau, 3/4 = sweep_k16 records/tau."""
+        pre-transformed triangles, 1/2 = render_mfma records/tau, 3/4 = sweep_k16 records/tau,
+        5 = the k5 form's per-triangle m.z residual bounds (float32 pairs)."""
         n = lib().rt2_scene_export(self._p, what, None, 0)
         if n < 0:
             raise RT2Error("rt2_scene_export: bad argument")
@@ -595,11 +596,12 @@ class Scene:
     def mfma_probe(self, layout: int, rays: np.ndarray):
         """The matrix filter's terms on the device (rt2_mfma_probe, test hook):
         rays (n, 8) float32 {o, best, d, 0}, n a multiple of 64; layout 0 =
-        16x16x32 (render_mfma), 1 = k16.  Returns (terms [n, n_pad, 5], frags
+        16x16x32 (render_mfma), 1 = k16, 2 = its 5-product form (k5).  Returns (terms [n, n_pad, 5], frags
         [n, 48] float16, rinfo [n, 8], accept [n, n_tris] bool)."""
         rays = np.ascontiguousarray(rays, dtype=np.float32)
         n = rays.shape[0]
-        n_pad = -(-self.n_tris // (32 if layout == 1 else 16)) * (32 if layout == 1 else 16)
+        g = 32 if layout >= 1 else 16
+        n_pad = -(-self.n_tris // g) * g
         terms = np.zeros((n, n_pad, 5), dtype=np.float32)
         frags = np.zeros((n, 48), dtype=np.uint16)
         rinfo = np.zeros((n, 8), dtype=np.float32)

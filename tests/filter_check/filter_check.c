@@ -221,8 +221,14 @@ static int mfma_record(f3 a, f3 e0, f3 e1, f3 n, double slot[MQ][32], double* ta
 #ifndef YMMA_TS
 #define YMMA_TS 0x1p-12f
 #endif
+/* k5 (rt2_mfma.h MfmaSpec::k5, with ymma): U, -V, X leave out their m.z
+ * slots 16 and 17 (coefficient hi x ray lo, coefficient lo x ray hi) and the
+ * threshold grows by the bound CH max|ray lo| + CL max|ray hi| (CH, CL: the
+ * record's largest |slot 16|, |slot 17| over U, -V, X), padded by 2^-10.  The
+ * wave's maxima are at least this ray's own values; the check uses exactly
+ * those (the smallest bound a wave can have). */
 static int pass_mfma(f3 o, f3 d, double slot[MQ][32], double tau, float As, float Ow, float Mw, float bestK,
-                     int ymma, float ts) {
+                     int ymma, float ts, int k5) {
     const f3 m = cross(d, o);
     const float ao = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
     const float am = fmaxf(fmaxf(fabsf(m.x), fabsf(m.y)), fabsf(m.z));
@@ -246,12 +252,18 @@ static int pass_mfma(f3 o, f3 d, double slot[MQ][32], double tau, float As, floa
     }
     ray[27] = ray[28] = sigma;
     ray[29] = ray[30] = ray[31] = 0.0;
-    const float Tl = (float)tau * Tw;
+    float Tl = (float)tau * Tw;
+    if (k5) {
+        float ch = 0.0f, cl = 0.0f;
+        for (int q = 0; q < 3; q++) ch = fmaxf(ch, (float)fabs(slot[q][16])), cl = fmaxf(cl, (float)fabs(slot[q][17]));
+        Tl += (ch * (float)fabs(ray[16]) + cl * (float)fabs(ray[17])) * 1.0009765625f;
+    }
     const float cd = (float)tau * Cw;
     float qv[MQ], qe[MQ];
     for (int q = 0; q < MQ; q++) {
         double s = q == 4 ? cd : 0.0, sa = q == 4 ? fabs(cd) : 0.0;
         for (int k = 0; k < 32; k++) {
+            if (k5 && q < 3 && (k == 16 || k == 17)) continue;  /* the products the 5-product form leaves out */
             const double p = ray[k] * slot[q][k];
             s += p;
             sa += fabs(p);
@@ -297,6 +309,7 @@ int main(int argc, char** argv) {
     long long accepts = 0, bad_old = 0, bad_new = 0, p_old = 0, p_new = 0, bad_plk = 0, p_plk = 0, p_plk_near = 0, p_old_near = 0;
     long long bad_mfma = 0, p_mfma = 0, n_mfma = 0, p_mfma_near = 0, n_mfma_near = 0;
     long long bad_y = 0, p_y = 0, p_y_near = 0;
+    long long bad_k5 = 0, p_k5 = 0, p_k5_near = 0;
     for (long long it = 0; it < n; it++) {
         const int kind = (int)(next64() % 6);
         const int far = (next64() % 4) == 0;  /* small triangle far from the origin */
@@ -366,8 +379,12 @@ int main(int argc, char** argv) {
             const float Ow = wk == 1 ? 0x1p20f * uni() : wk == 2 ? 2.0f * scale * uni() : 0.0f;
             const float Mw = wk == 3 ? 0x1p20f * uni() : 0.0f;
             const float As = inr ? fmaxf(Am, (next64() % 3) == 0 ? 0x1p20f * uni() : 0.0f) : 0x1p20f;
-            const int fm = pass_mfma(o, d, slot, tau, As, Ow, Mw, bestK, 0, 0x1p-10f);
-            const int fy = pass_mfma(o, d, slot, tau, As, Ow, Mw, bestK, 1, YMMA_TS);
+            const int fm = pass_mfma(o, d, slot, tau, As, Ow, Mw, bestK, 0, 0x1p-10f, 0);
+            const int fy = pass_mfma(o, d, slot, tau, As, Ow, Mw, bestK, 1, YMMA_TS, 0);
+            const int f5 = pass_mfma(o, d, slot, tau, As, Ow, Mw, bestK, 1, YMMA_TS, 1);
+            p_k5 += f5;
+            if (ex && !f5) bad_k5++;
+            if (!far && !wide && wk == 0 && inr) p_k5_near += f5;
             n_mfma++;
             p_mfma += fm;
             p_y += fy;
@@ -383,9 +400,9 @@ int main(int argc, char** argv) {
         if (ex && !fo) bad_old++;
         if (ex && !fn) bad_new++;
     }
-    printf("%lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld\n", n, accepts, bad_old,
-           bad_new, p_old, p_new, bad_plk, p_plk, bad_mfma, p_mfma, n_mfma, p_mfma_near, n_mfma_near, bad_y, p_y,
-           p_y_near);
+    printf("%lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld\n", n, accepts,
+           bad_old, bad_new, p_old, p_new, bad_plk, p_plk, bad_mfma, p_mfma, n_mfma, p_mfma_near, n_mfma_near, bad_y,
+           p_y, p_y_near, bad_k5, p_k5, p_k5_near);
     fprintf(stderr, "near-origin draws: pass_old %lld pass_plk %lld\n", p_old_near, p_plk_near);
     return 0;
 }

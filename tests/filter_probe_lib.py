@@ -83,12 +83,29 @@ def fma32(x, y, z):
     return (x.astype(np.float64) * y.astype(np.float64) + z.astype(np.float64)).astype(np.float32)
 
 
-def analyse(terms, frags, rinfo, accept, B, coef, tau, rays, T_tau):
+def k5_bounds(B):
+    """The k5 form's per-triangle bounds (prep_mfma_k16 bnd_out): the largest
+    |slot 16| and |slot 17| of U, -V, X (float32)."""
+    return (np.abs(B[:, :3, 16]).max(1).astype(np.float32), np.abs(B[:, :3, 17]).max(1).astype(np.float32))
+
+
+def analyse(terms, frags, rinfo, accept, B, coef, tau, rays, T_tau, bnd=None):
     """Measures one probe run.  Returns a dict of statistics and the arrays of
-    violations (empty when the filter is conservative)."""
+    violations (empty when the filter is conservative).  bnd = (CH, CL) per
+    triangle: the 5-product form (k5), whose U, -V, X leave out slots 16/17 and
+    whose threshold grows by (CH max|ray slot 16| + CL max|ray slot 17|)(1 +
+    2^-10), the maxima over the ray's wave of 64 (sweep_k16)."""
     n_tris = accept.shape[1]
     live = rinfo[:, 0] == 1.0
     hw = terms[live][:, :n_tris, :].astype(np.float64)          # (R, T, 5)
+    if bnd is not None:
+        B = B.copy()
+        B[:, :3, 16:18] = 0.0  # the products the k5 form leaves out
+        fw = np.abs(frags.astype(np.float32)).reshape(-1, 64, 48)
+        zlo = np.repeat(fw[:, :, 16].max(1), 64)[live]
+        zhi = np.repeat(fw[:, :, 17].max(1), 64)[live]
+        ch, cl = bnd[0][:n_tris], bnd[1][:n_tris]
+        Bk = ((ch[None, :] * zlo[:, None] + cl[None, :] * zhi[:, None]) * np.float32(1.0009765625)).astype(np.float32)
     fr = frags[live].astype(np.float64)
     A_main = fr[:, :32]
     A_y = np.concatenate([np.zeros((len(fr), 16)), fr[:, 32:48]], 1)
@@ -122,7 +139,13 @@ def analyse(terms, frags, rinfo, accept, B, coef, tau, rays, T_tau):
     ideal_y = vy @ ct[:, 3, :].T
     ideal = np.concatenate([ideal, ideal_y[..., None]], 2)
     Tl = (T_tau[None, :n_tris].astype(np.float32) * Tw[:, None].astype(np.float32)).astype(np.float32)
-    tot_ratio = np.abs(hw - ideal) / Tl[..., None].astype(np.float64)
+    dev = np.abs(hw - ideal)
+    if bnd is not None:
+        dev[..., :3] = np.maximum(dev[..., :3] - Bk[..., None].astype(np.float64), 0.0)  # beyond the k5 bound
+    tot_ratio = dev / Tl[..., None].astype(np.float64)
+    T0 = Tl
+    if bnd is not None:
+        Tl = (Tl + Bk).astype(np.float32)  # sweep_k16: Tl += (bnd.x zlo + bnd.y zhi) (1 + 2^-10)
 
     # conservativeness: accepted => every term <= Tl (the kernels' integer max)
     bits = hw.astype(np.float32).view(np.int32).max(-1)
@@ -141,6 +164,9 @@ def analyse(terms, frags, rinfo, accept, B, coef, tau, rays, T_tau):
         "total_err_by_term_max_over_T": {Q_NAMES[q]: float(tot_ratio[..., q].max()) for q in range(5)},
         "violations": int(len(violations)),
     }
+    if bnd is not None:
+        g = (Bk / T0).astype(np.float64)
+        out["k5_bound_over_T"] = {"max": float(g.max()), "mean": float(g.mean()), "p99": float(np.percentile(g, 99))}
     return out, violations
 
 

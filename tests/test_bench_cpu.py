@@ -98,6 +98,11 @@ def test_roofline_matrix_kernel():
     rf = bench.roofline(segs * n, 0, kern_ms, segs, n, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp")
     assert rf["achieved"] == pytest.approx(bench.MFMA_K16_FLOP_PER_PAIR * segs * 1216 / (kern_ms * 1e-3) / 1e12,
                                            rel=1e-3)
+    # its 5-product form: 160 FLOP per pair
+    rf = bench.roofline(segs * n, 0, kern_ms, segs, n, "mfma/256/k5/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp")
+    assert rf["achieved"] == pytest.approx(bench.MFMA_K5_FLOP_PER_PAIR * segs * 1216 / (kern_ms * 1e-3) / 1e12,
+                                           rel=1e-3)
+    assert "5-product" in rf["flop_model"]
 
 
 def test_kernel_labels():

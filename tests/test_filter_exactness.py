@@ -134,3 +134,37 @@ def test_harness_detects_a_wrong_ymma_filter(tmp_path, old, new):
     subprocess.run(["gcc", "-O2", "-std=c11", "-ffp-contract=off", "-o", exe, str(p), "-lm"], check=True)
     (bad, _, _), _ = _run_mfma_y(exe, 1_000_000, 1)
     assert bad > 0
+
+
+def _run_k5(exe, n, seed):
+    """(violations, passes, passes at ordinary scales) of the 5-product form
+    (MfmaSpec::k5) and the same three figures of the 8-product ymma form, on
+    the same draws."""
+    out = subprocess.run([exe, str(n), str(seed)], check=True, capture_output=True, text=True).stdout
+    v = tuple(map(int, out.split()))
+    return v[16:19], v[13:16]
+
+
+@pytest.mark.parametrize("seed", [8, 9])
+def test_matrix_filter_k5_conservative(checker, seed):
+    """The 5-product form: U, -V, X without their m.z slots 16/17, the
+    threshold raised by the per-(wave, triangle) bound of what is left out.
+    No accepted pair is skipped, and it passes at most a few percent more
+    pairs than the 8-product form on the same draws."""
+    (bad, passes, p_near), (bad_y, passes_y, p_near_y) = _run_k5(checker, 2_000_000, seed)
+    assert bad == 0 and bad_y == 0
+    assert passes_y <= passes <= passes_y * 1.03 and p_near <= p_near_y * 1.03
+
+
+def test_harness_detects_k5_without_its_bound(tmp_path):
+    """Leaving out the m.z slots without raising the threshold skips accepted
+    pairs: the bound is necessary, and the harness sees its absence."""
+    src = open(SRC).read()
+    old = "    if (k5) {\n        float ch"
+    assert old in src
+    p = tmp_path / "mut.c"
+    p.write_text(src.replace(old, "    if (0) {\n        float ch"))
+    exe = str(tmp_path / "mut")
+    subprocess.run(["gcc", "-O2", "-std=c11", "-ffp-contract=off", "-o", exe, str(p), "-lm"], check=True)
+    (bad, _, _), _ = _run_k5(exe, 1_000_000, 1)
+    assert bad > 0

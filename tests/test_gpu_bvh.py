@@ -189,11 +189,11 @@ def test_bvh2_big_leaves_and_single_node(rt2mod, oraclemod, torch_cuda):
 
 
 @pytest.mark.parametrize("traversal", ["brute", "bvh"])
-@pytest.mark.parametrize("brute_variant", [0, 86], ids=["auto-k16", "tiled"])
+@pytest.mark.parametrize("brute_variant", [0, 86], ids=["auto-k5", "tiled"])
 def test_config_E_million_triangles(rt2mod, oraclemod, config_scene, torch_cuda, traversal, brute_variant):
     """Config E (1,000,014 triangles, mirror box, 16 bounces) at a small image:
     both traversals bit-exact against the oracle; brute force by the automatic
-    choice (the k16 matrix kernel, variant 200) and the scalar LDS-tiled kernel."""
+    choice (the 5-product k16 matrix kernel, variant 227) and the scalar LDS-tiled kernel."""
     if traversal == "bvh" and brute_variant:
         pytest.skip("the brute-force variant does not apply to the BVH traversal")
     sd, spec = config_scene("E")

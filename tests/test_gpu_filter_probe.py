@@ -55,7 +55,7 @@ def _materials(rt2mod):
     return sd.materials()
 
 
-@pytest.mark.parametrize("layout", [0, 1], ids=["f16x32", "k16"])
+@pytest.mark.parametrize("layout", [0, 1, 2], ids=["f16x32", "k16", "k5"])
 @pytest.mark.parametrize("kind", KINDS)
 def test_filter_terms_on_hardware(rt2mod, torch_cuda, kind, layout):
     rng = np.random.default_rng(100 + KINDS.index(kind))
@@ -69,14 +69,21 @@ def test_filter_terms_on_hardware(rt2mod, torch_cuda, kind, layout):
     else:
         B = fpl.records_k16(scene.export(3, np.uint16), len(V))
         T_tau = scene.export(4, np.float32)
+    bnd = None
+    if layout == 2:
+        # the device's k5 bounds are the records' largest |slot 16|, |slot 17| of U, -V, X
+        dev = scene.export(5, np.float32).reshape(-1, 2)[:len(V)]
+        bnd = fpl.k5_bounds(B)
+        np.testing.assert_array_equal(dev[:, 0], bnd[0])
+        np.testing.assert_array_equal(dev[:, 1], bnd[1])
     # the device's records are the host's coefficients split into f16 hi/lo slots
     np.testing.assert_array_equal(T_tau[:len(V)], tau.astype(np.float32))
     hi = (coef * tau[:, None, None]).astype(np.float32).astype(np.float16).astype(np.float64)
     np.testing.assert_array_equal(B[:, :4, 0:27:3], hi[:, :4, :9])
     terms, frags, rinfo, accept = scene.mfma_probe(layout, rays)
-    st, viol = fpl.analyse(terms, frags, rinfo, accept, B, coef, tau, rays, T_tau)
+    st, viol = fpl.analyse(terms, frags, rinfo, accept, B, coef, tau, rays, T_tau, bnd)
     st["triangles_in_range"] = int(ok.sum())
-    _results[f"{kind}/{['f16x32', 'k16'][layout]}"] = st
+    _results[f"{kind}/{['f16x32', 'k16', 'k5'][layout]}"] = st
     assert st["rays_in_range"] >= len(rays) // 2
     assert st["accepted_pairs"] > 0
     assert st["violations"] == 0, f"reference-accepted pairs rejected by the filter: {viol[:10]}"
@@ -144,7 +151,7 @@ def near_threshold_scene(rt2mod):
     return sd
 
 
-@pytest.mark.parametrize("variant", [150, 152, 200, 206])
+@pytest.mark.parametrize("variant", [150, 152, 200, 206, 227, 228])
 def test_near_threshold_scene_bit_exact(rt2mod, oraclemod, torch_cuda, variant):
     if not rt2mod.has_variant(variant):
         pytest.skip(f"variant {variant} not in this build")

@@ -100,8 +100,8 @@ def _last_variant(rt2mod, scene):
     return rt2mod.lib().rt2_variant_name(lv.value).decode()
 
 
-AUTO_MFMA = "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"  # variant 200 (the k16 sweep)
-AUTO_MFMA_SLAB = "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp"  # variant 206: < 1.5 items per lane
+AUTO_MFMA = "mfma/256/k5/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"  # variant 227 (the 5-product k16 form)
+AUTO_MFMA_SLAB = "mfma/256/k5/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp"  # variant 228: < 1.5 items per lane
 
 
 def test_auto_variant_large_scene(rt2mod, config_scene, torch_cuda):
@@ -329,7 +329,7 @@ def test_frame_split_identical(rt2mod, oraclemod, config_scene, torch_cuda, trav
 # forced) and, in an experiment build, the A/B
 # variants (masked/plk filters, resident LDS, cooperative and team tail modes,
 # split waves, the round-1 slab kernels, occupancy hints)
-BRUTE_VARIANTS = [0, 86, 92, 150, 152, 200, 206, 136] + ([137, 138, 139, 140, 143, 144, 145, 146] if EXPERIMENTS else []) + ([22, 24, 28, 52, 64, 65, 66, 67, 68, 70, 71, 72, 73, 74, 76, 79, 80, 84, 85, 87, 89, 95, 97, 101, 104, 106,
+BRUTE_VARIANTS = [0, 86, 92, 150, 152, 200, 206, 227, 228, 136] + ([137, 138, 139, 140, 143, 144, 145, 146] if EXPERIMENTS else []) + ([22, 24, 28, 52, 64, 65, 66, 67, 68, 70, 71, 72, 73, 74, 76, 79, 80, 84, 85, 87, 89, 95, 97, 101, 104, 106,
                                  90] if EXPERIMENTS else [])
 
 
