@@ -63,6 +63,8 @@ struct MfmaSpec {
     bool compact = false;   // k16: <= 32 live rays move to lanes 0..31 and the second 32-ray block is skipped
     bool k5 = false;        // k16: U, -V, X from the first K-half only (5 products per 32-ray block instead of 8);
                             // the two m.z slots left out are bounded per (wave, triangle) and added to the threshold
+    bool no_tn = false;     // k5 experiment: no -tn term (4 products per block; the filter stays conservative,
+                            // it only passes more pairs to the exact phase)
     int serial = 0;         // k16: scheduling fences per 32-ray block: 1 = U V X products | their max | -tn Y
                             // products | the rest (48 accumulator VGPRs live); 2 = all 8 products | the reduction;
                             // 3 = 1 without the fence between the blocks; 4 = 3 without the fence at the group end
@@ -593,6 +595,7 @@ __device__ __forceinline__ K16Terms k16_terms(const h8& a0, const h8& a1, const 
     return r;
 }
 
+__device__ __forceinline__ f16v Y_unused_init() { return f16v{}; }
 template <MfmaSpec S, class SH>
 __device__ __forceinline__ bool sweep_k16_pipe(const RenderParams& p, SH& sh, const f3& o, const f3& d, float& best,
                                                int& bi, float& bestK, MfmaDiag& dg);
@@ -722,7 +725,8 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, SH& sh, const f
                         u3[i] = min(min(__float_as_int(U[i]), __float_as_int(V[i])), __float_as_int(X[i]));
                 }
                 __builtin_amdgcn_sched_barrier(0);
-                const f16v T = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[R], b[6], zero, 0, 0, 0);
+                f16v T = Y_unused_init();
+                if constexpr (!S.no_tn) T = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[R], b[6], zero, 0, 0, 0);
                 const f16v Y = __builtin_amdgcn_mfma_f32_32x32x16_f16(y1[R], b[6], zero, 0, 0, 0);
                 if constexpr (S.sol == 7) {
                     // marginal-cost probe: the block's 8 products once more, one chain (sunk per group)
@@ -741,8 +745,12 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, SH& sh, const f
                     }
                 }
 #pragma unroll
-                for (int i = 0; i < 16; i++)
-                    tmin = min(tmin, max(max(t3[i], __float_as_int(T[i])), __float_as_int(Y[i])));
+                for (int i = 0; i < 16; i++) {
+                    if constexpr (S.no_tn)
+                        tmin = min(tmin, max(t3[i], __float_as_int(Y[i])));
+                    else
+                        tmin = min(tmin, max(max(t3[i], __float_as_int(T[i])), __float_as_int(Y[i])));
+                }
                 if constexpr (S.sol == 6) {
 #pragma unroll
                     for (int i = 0; i < 16; i++)

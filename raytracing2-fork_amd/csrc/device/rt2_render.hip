@@ -683,8 +683,10 @@ const Variant kVariants[] = {
     RT2_VARIANT(214, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.pipe = true; x.diag = true; x.waves = 2; return x; }()>, 256, "mfma/256/k16/coop8/w2/imax/minred/ymma/t12/llds/ser4/cmp/pipe/diag"),
     RT2_VARIANT(222, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16W4; x.diag = true; return x; }()>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp/diag"),
     // the 5-product form (MfmaSpec::k5): U, -V, X from the first K-half, the m.z residual bounded in the threshold
-    RT2_VARIANT(229, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.k5 = true; x.diag = true; return x; }()>, 256, "mfma/256/k5/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp/diag"),
-    RT2_VARIANT(230, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.k5 = true; x.waves = 4; return x; }()>, 256, "mfma/256/k5/coop8/w4/imax/minred/ymma/t12/llds/ser4/cmp"),
+    RT2_VARIANT(231, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5; x.no_tn = true; return x; }()>, 256, "mfma/256/k5/notn/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"),
+    RT2_VARIANT(232, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5; x.no_tn = true; x.diag = true; return x; }()>, 256, "mfma/256/k5/notn/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp/diag"),
+    RT2_VARIANT(229, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5; x.diag = true; return x; }()>, 256, "mfma/256/k5/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp/diag"),
+    RT2_VARIANT(230, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5; x.waves = 4; return x; }()>, 256, "mfma/256/k5/coop8/w4/imax/minred/ymma/t12/llds/ser4/cmp"),
     // the k16 kernels without the workgroup's per-segment barrier (waves run free)
     RT2_VARIANT(223, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.lockstep = false; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp/free"),
     RT2_VARIANT(224, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16W4; x.lockstep = false; return x; }()>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp/free"),
