@@ -60,6 +60,7 @@ MFMA_F16_PEAK_TFLOPS = 2500.0  # MI355X dense F16/BF16 matrix peak (MI355X_MICRO
 MFMA_FLOP_PER_PAIR = 320   # render_mfma 16x16x32 form: 5 quantities x 32 k-slots x 2 per (ray, triangle) pair
 MFMA_K16_FLOP_PER_PAIR = 256  # the k16 sweep: 8 v_mfma_f32_32x32x16_f16 (32x32x16x2 FLOP each) per 1,024 pairs
 MFMA_K5_FLOP_PER_PAIR = 160   # its 5-product form (MfmaSpec::k5): 5 v_mfma_f32_32x32x16_f16 per 1,024 pairs
+MFMA_K5_NOTN_FLOP_PER_PAIR = 128  # ... without the -tn term (small scenes): 4 per 1,024 pairs
 TARGET_RATIO = 10.0        # north star: >= 10x the CPU reference at config C on 1 GPU
 KERNEL_FILES = {"mfma": "render_mfma", "massist": "render_assist", "smem": "render_smem", "split": "render_split", "tiled": "render_tiled", "assist": "render_assist",
                 "resident": "render_resident", "bvh4": "render_bvh4", "bvh3": "render_bvh3", "bvh2": "render_bvh2",
@@ -210,9 +211,13 @@ def roofline(tests, visits, kern_ms, segments=0, n_tris=0, variant=None):
         k16 = "/k16/" in variant or k5
         group = 32 if k16 else 16
         pairs = segments * (-(-int(n_tris) // group) * group)
-        fpp = MFMA_K5_FLOP_PER_PAIR if k5 else MFMA_K16_FLOP_PER_PAIR if k16 else MFMA_FLOP_PER_PAIR
+        notn = k5 and "/notn/" in variant
+        fpp = (MFMA_K5_NOTN_FLOP_PER_PAIR if notn else MFMA_K5_FLOP_PER_PAIR if k5 else MFMA_K16_FLOP_PER_PAIR if k16
+               else MFMA_FLOP_PER_PAIR)
         mf = fpp * pairs / (kern_ms * 1e-3) / 1e12
-        model = ("160 x (ray, triangle) pairs: the 5-product k16 form's 5 v_mfma_f32_32x32x16_f16 per 32 rays x 32 "
+        model = ("128 x (ray, triangle) pairs: the 5-product k16 form without -tn, 4 v_mfma_f32_32x32x16_f16 per "
+                 "32 rays x 32 triangles (U, -V, X, Y: one K-half each), triangles padded to 32" if notn else
+                 "160 x (ray, triangle) pairs: the 5-product k16 form's 5 v_mfma_f32_32x32x16_f16 per 32 rays x 32 "
                  "triangles (U, -V, X, -tn, Y: one K-half each), triangles padded to 32" if k5 else
                  "256 x (ray, triangle) pairs: the k16 sweep's 8 v_mfma_f32_32x32x16_f16 per 32 rays x 32 "
                  "triangles (U, -V, X: two K-halves each; -tn, Y: one), triangles padded to 32"

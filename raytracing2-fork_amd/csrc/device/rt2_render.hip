@@ -568,6 +568,16 @@ constexpr MfmaSpec kMfmaK5W4 = [] {
     x.k5 = true;
     return x;
 }();
+constexpr MfmaSpec kMfmaK5NoTn = [] {
+    MfmaSpec x = kMfmaK5;
+    x.no_tn = true;
+    return x;
+}();
+constexpr MfmaSpec kMfmaK5NoTnW4 = [] {
+    MfmaSpec x = kMfmaK5W4;
+    x.no_tn = true;
+    return x;
+}();
 constexpr Bvh3Spec kBvhDefault{.block = 256, .thresh = 16, .slab = Slab::Markstein, .waves = 5, .diag = false};
 
 #ifdef RT2_EXPERIMENTS
@@ -631,6 +641,11 @@ const Variant kVariants[] = {
     // the left-out m.z slots bounded in the threshold; 3 waves per SIMD, and 4 for launches with < 1.5 items per lane
     RT2_VARIANT(227, K_MFMA, render_mfma<kMfmaK5>, 256, "mfma/256/k5/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"),
     RT2_VARIANT(228, K_MFMA, render_mfma<kMfmaK5W4>, 256, "mfma/256/k5/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
+    // scenes of <= 8,192 triangles (records L2-resident): the same without the -tn term (4 products per block;
+    // config B 195 vs 214 ms for 227, config E sample +9 %: there the term pays), 4 waves (packed path state)
+    // or 3 when the packed fields do not hold the image / rays / bounces
+    RT2_VARIANT(233, K_MFMA, render_mfma<kMfmaK5NoTnW4>, 256, "mfma/256/k5/notn/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
+    RT2_VARIANT(231, K_MFMA, render_mfma<kMfmaK5NoTn>, 256, "mfma/256/k5/notn/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"),
 #ifdef RT2_EXPERIMENTS
     RT2_VARIANT(160, K_MFMA, render_mfma<k16_spec(3)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12"),
     RT2_VARIANT(161, K_MFMA, render_mfma<k16_spec(4)>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12"),
@@ -683,8 +698,7 @@ const Variant kVariants[] = {
     RT2_VARIANT(214, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.pipe = true; x.diag = true; x.waves = 2; return x; }()>, 256, "mfma/256/k16/coop8/w2/imax/minred/ymma/t12/llds/ser4/cmp/pipe/diag"),
     RT2_VARIANT(222, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16W4; x.diag = true; return x; }()>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp/diag"),
     // the 5-product form (MfmaSpec::k5): U, -V, X from the first K-half, the m.z residual bounded in the threshold
-    RT2_VARIANT(231, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5; x.no_tn = true; return x; }()>, 256, "mfma/256/k5/notn/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"),
-    RT2_VARIANT(232, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5; x.no_tn = true; x.diag = true; return x; }()>, 256, "mfma/256/k5/notn/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp/diag"),
+    RT2_VARIANT(232, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTn; x.diag = true; return x; }()>, 256, "mfma/256/k5/notn/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp/diag"),
     RT2_VARIANT(229, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5; x.diag = true; return x; }()>, 256, "mfma/256/k5/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp/diag"),
     RT2_VARIANT(230, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5; x.waves = 4; return x; }()>, 256, "mfma/256/k5/coop8/w4/imax/minred/ymma/t12/llds/ser4/cmp"),
     // the k16 kernels without the workgroup's per-segment barrier (waves run free)
@@ -782,11 +796,12 @@ constexpr int kDefaultBvh = 109;
 constexpr int kLargeScene = 86;  // tiled/512/max3f4: LDS tiles above kSmemMaxTris triangles
 constexpr int kSlab = 92;        // assist12/max3f8/w6: fewer than 4 items per lane (multi-GPU slabs)
 constexpr int kMfmaSlabMaxTris = 8192;
-constexpr int kMfmaSlab = 228;  // 4 waves per SIMD: more resident lanes for launches with < 1.5 items per 3-wave
-                                // lane (config B's 1/8 slab: 32.1 vs 38.6 ms for variant 227; k16: 39.1 vs 41.4 ms)
+constexpr int kMfmaSmall = 233;    // <= kMfmaSlabMaxTris triangles: k5 without -tn, 4 waves (packed path state)
+constexpr int kMfmaSmallW3 = 231;  // ... 3 waves, when the packed fields cannot hold the launch
 constexpr int kMfma = 227;  // mfma/.../k5/...: the matrix-core filter on v_mfma_f32_32x32x16_f16, 5 products per
                             // 32-ray block (DESIGN.md "The 5-product form"): config B 214 vs 261 ms for the 8-product
-                            // k16 sweep (variant 200), config C sample 1.85 vs 2.08 s, config E sample 2.42 vs 2.63 s
+                            // k16 sweep (variant 200), config C sample 1.85 vs 2.08 s, config E sample 2.42 vs 2.63 s;
+                            // scenes above kMfmaSlabMaxTris triangles (smaller ones: kMfmaSmall)
 
 constexpr bool is_bvh(int kind) { return kind >= K_BVH && kind <= K_BVH4; }
 
@@ -1031,19 +1046,21 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
             // slabs' tails) and every scene size: config E's 1M triangles too
             // (3.9 vs 6.9 s for kLargeScene on a 480x270 sample)
             vi = kMfma;
-            // few items per lane (the 1/8 slab of config B): the 4-wave build's
-            // extra lanes shorten the last round; it packs the path state into
-            // 16-bit fields (x, y, rays per pixel) and 12 bits of bounce count.
-            // Only while the records stay L2-resident: at config C's 100k
-            // triangles the fourth wave costs more than its lanes gain (a
-            // 480x270x2 sample, 1.3 items per lane: 3.13 vs 2.13 s)
-            const Variant* W4 = find_variant(kMfmaSlab);
-            int occ3 = 0;
-            HIPCHECK(variant_occupancy(*find_variant(kMfma), &occ3, 0));
-            const double ipl3 = (double)p.n_items / ((double)s->num_cus * std::max(occ3, 1) * 256.0);
-            if (W4 && ipl3 < 1.5 && s->n_tris <= kMfmaSlabMaxTris && u->width <= 65535 && u->height <= 65535 && u->maxBounceCount <= 4095 &&
-                u->numRaysPerPixel <= 65535)
-                vi = kMfmaSlab;
+            // scenes whose records stay L2-resident (<= 8,192 triangles: config
+            // B): without the -tn term, whose exact tests cost less there than
+            // its product (config B 195 vs 214 ms; on config E's closed mirror
+            // box it pays: +9 % without it), and at 4 waves per SIMD, which
+            // packs the path state into 16-bit fields (x, y, rays per pixel)
+            // and 12 bits of bounce count: whole images and rank slabs alike
+            // (config B 195 vs 200 ms at 3 waves; 1/8 slab 29.4 vs 34.6 ms).
+            // At config C's 100k triangles the fourth wave costs more than its
+            // lanes gain (a 480x270x2 sample, 1.3 items per lane: 3.13 vs
+            // 2.13 s for the k16 sweep)
+            if (s->n_tris <= kMfmaSlabMaxTris) {
+                const bool packed = u->width <= 65535 && u->height <= 65535 && u->maxBounceCount <= 4095 &&
+                                    u->numRaysPerPixel <= 65535;
+                vi = packed && find_variant(kMfmaSmall) ? kMfmaSmall : kMfmaSmallW3;
+            }
         } else if (vi == kDefaultBrute) {
             // scenes outside the matrix filter's range (mfma_ok = 0):
             // items per resident lane decide the tail: a lane ends on a whole

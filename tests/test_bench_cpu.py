@@ -103,6 +103,9 @@ def test_roofline_matrix_kernel():
     assert rf["achieved"] == pytest.approx(bench.MFMA_K5_FLOP_PER_PAIR * segs * 1216 / (kern_ms * 1e-3) / 1e12,
                                            rel=1e-3)
     assert "5-product" in rf["flop_model"]
+    rf = bench.roofline(segs * n, 0, kern_ms, segs, n, "mfma/256/k5/notn/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp")
+    assert rf["achieved"] == pytest.approx(bench.MFMA_K5_NOTN_FLOP_PER_PAIR * segs * 1216 / (kern_ms * 1e-3) / 1e12,
+                                           rel=1e-3)
 
 
 def test_kernel_labels():

@@ -101,14 +101,15 @@ def _last_variant(rt2mod, scene):
 
 
 AUTO_MFMA = "mfma/256/k5/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"  # variant 227 (the 5-product k16 form)
-AUTO_MFMA_SLAB = "mfma/256/k5/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp"  # variant 228: < 1.5 items per lane
+AUTO_SMALL = "mfma/256/k5/notn/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp"  # 233: <= 8,192 triangles
+AUTO_SMALL_W3 = "mfma/256/k5/notn/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"  # 231: packed fields too small
 
 
 def test_auto_variant_large_scene(rt2mod, config_scene, torch_cuda):
     """Scenes whose matrix-filter records outgrow an XCD's L2 (config C: 100k
-    triangles, 22 MB of k16 records) run the same k16 matrix kernel, and the
-    3-wave build even below 1.5 items per lane (this small image): the 4-wave
-    build serves only scenes of <= 8,192 triangles."""
+    triangles, 22 MB of k16 records) run the 5-product form with its -tn term
+    at 3 waves per SIMD, even below 1.5 items per lane (this small image): the
+    4-wave build without -tn serves only scenes of <= 8,192 triangles."""
     sd, spec = config_scene("C")
     u = rt2mod.offline_uniforms(64, 36, spec.bounces, 1, sd.num_triangles)
     scene = rt2mod.Scene(sd, 0)
@@ -117,17 +118,17 @@ def test_auto_variant_large_scene(rt2mod, config_scene, torch_cuda):
 
 
 def test_auto_variant_packed_state_limits(rt2mod, oraclemod, config_scene, torch_cuda):
-    """Below 1.5 items per lane the launcher takes the 4-wave k16 build, whose
-    path state packs the bounce count into 12 bits; a bounce limit above 4095
-    keeps the 3-wave build — same image either way."""
+    """Small scenes run the 4-wave build, whose path state packs the bounce
+    count into 12 bits; a bounce limit above 4095 takes the 3-wave build of
+    the same form — same image either way."""
     sd, spec = config_scene("B")
     u = rt2mod.offline_uniforms(40, 24, spec.bounces, 3, sd.num_triangles)
     scene = rt2mod.Scene(sd, 0)
     img = scene.render_host(u, 0, 1)
-    assert _last_variant(rt2mod, scene) == AUTO_MFMA_SLAB
+    assert _last_variant(rt2mod, scene) == AUTO_SMALL
     u.maxBounceCount = 5000
     img2 = scene.render_host(u, 0, 1)
-    assert _last_variant(rt2mod, scene) == AUTO_MFMA
+    assert _last_variant(rt2mod, scene) == AUTO_SMALL_W3
     ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(24), 0, 1)
     assert_exact(img2, ref, "5000 bounces")
     u.maxBounceCount = spec.bounces
@@ -144,8 +145,8 @@ def test_auto_variant_by_items_per_lane(rt2mod, config_scene, torch_cuda):
     u = rt2mod.offline_uniforms(spec.width, spec.height, spec.bounces, spec.rays, sd.num_triangles)
     scene = rt2mod.Scene(sd, 0)
     full = scene.render_host(u, 0, 1)
-    assert _last_variant(rt2mod, scene) == AUTO_MFMA
-    for n, want in ((2, AUTO_MFMA), (4, AUTO_MFMA), (8, AUTO_MFMA_SLAB)):
+    assert _last_variant(rt2mod, scene) == AUTO_SMALL
+    for n, want in ((2, AUTO_SMALL), (4, AUTO_SMALL), (8, AUTO_SMALL)):
         sh = rt2mod.shard(1, n - 1, n)
         img = scene.render_host(u, 0, 1, sh)
         assert _last_variant(rt2mod, scene) == want
@@ -329,7 +330,7 @@ def test_frame_split_identical(rt2mod, oraclemod, config_scene, torch_cuda, trav
 # forced) and, in an experiment build, the A/B
 # variants (masked/plk filters, resident LDS, cooperative and team tail modes,
 # split waves, the round-1 slab kernels, occupancy hints)
-BRUTE_VARIANTS = [0, 86, 92, 150, 152, 200, 206, 227, 228, 136] + ([137, 138, 139, 140, 143, 144, 145, 146] if EXPERIMENTS else []) + ([22, 24, 28, 52, 64, 65, 66, 67, 68, 70, 71, 72, 73, 74, 76, 79, 80, 84, 85, 87, 89, 95, 97, 101, 104, 106,
+BRUTE_VARIANTS = [0, 86, 92, 150, 152, 200, 206, 227, 228, 231, 233, 136] + ([137, 138, 139, 140, 143, 144, 145, 146] if EXPERIMENTS else []) + ([22, 24, 28, 52, 64, 65, 66, 67, 68, 70, 71, 72, 73, 74, 76, 79, 80, 84, 85, 87, 89, 95, 97, 101, 104, 106,
                                  90] if EXPERIMENTS else [])
 
 
