@@ -1,14 +1,16 @@
 #!/bin/bash
 # PMC passes for the bench's render kernel (one counter group per rocprofv3 run,
-# --kernel-trace/--pmc only; no sys/runtime trace).  Output: gpurun_out/pmc_<name>/
+# --kernel-trace/--pmc only; no sys/runtime trace).  Output: ${PMC_OUT:-gpurun_out}/pmc_<name>/
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 ARGS="--no-cpu-baseline --no-alt --no-config-c --steps 2 --warmup 1 ${BENCH_ARGS}"
+OUTD="$GRAFT_REPO_ROOT/${PMC_OUT:-gpurun_out}"
+mkdir -p "$OUTD"
 run() {
   local name=$1; shift
-  timeout -k 10 300 rocprofv3 --pmc "$@" --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_$name" -o run \
-    -- python3 "$GRAFT_REPO_ROOT/bench.py" $ARGS > "$GRAFT_REPO_ROOT/gpurun_out/pmc_$name.log" 2>&1
+  timeout -k 10 300 rocprofv3 --pmc "$@" --output-format csv -d "$OUTD/pmc_$name" -o run \
+    -- python3 "$GRAFT_REPO_ROOT/bench.py" $ARGS > "$OUTD/pmc_$name.log" 2>&1
 }
 run fetch FETCH_SIZE && \
 run write WRITE_SIZE && \
