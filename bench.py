@@ -57,6 +57,7 @@ BVH_RECORD_BYTES = 64      # BVH: one child-pair record per interior visit (both
 BVH_TRI_BYTES = 48         # BVH: one pre-transformed triangle record per leaf test
 L2_PEAK_GBS = 34500.0      # MI355X_MICROARCH.md §L2: ≈34.5 TB/s aggregate
 MFMA_F16_PEAK_TFLOPS = 2500.0  # MI355X dense F16/BF16 matrix peak (MI355X_MICROARCH.md; no sparsity)
+MFMA_F16_SUSTAINED_TFLOPS = 1240.0  # measured: 16 v_mfma_f32_32x32x16_f16 per 417-450 ns per SIMD at 2-4 waves (1.19-1.29 PF; overlap probe)
 MFMA_FLOP_PER_PAIR = 320   # render_mfma 16x16x32 form: 5 quantities x 32 k-slots x 2 per (ray, triangle) pair
 MFMA_K16_FLOP_PER_PAIR = 256  # the k16 sweep: 8 v_mfma_f32_32x32x16_f16 (32x32x16x2 FLOP each) per 1,024 pairs
 MFMA_K5_FLOP_PER_PAIR = 160   # its 5-product form (MfmaSpec::k5): 5 v_mfma_f32_32x32x16_f16 per 1,024 pairs
@@ -225,6 +226,12 @@ def roofline(tests, visits, kern_ms, segments=0, n_tris=0, variant=None):
                              "padded to 16)")
         rf.update({"bound": "mfma", "achieved": round(mf, 3), "peak": MFMA_F16_PEAK_TFLOPS,
                    "frac": round(mf / MFMA_F16_PEAK_TFLOPS, 4),
+                   "pairs_per_s": float(f"{pairs / (kern_ms * 1e-3):.4e}"),
+                   "matrix_pipe_sustained": {"value": MFMA_F16_SUSTAINED_TFLOPS, "unit": "TFLOP/s",
+                                             "frac_of_peak": round(MFMA_F16_SUSTAINED_TFLOPS / MFMA_F16_PEAK_TFLOPS, 3),
+                                             "note": "v_mfma_f32_32x32x16_f16 alone on random f16 operands, 2-4 waves "
+                                                     "per SIMD (scripts/overlap_probe.hip, profiles/r03_overlap_probe"
+                                                     ".jsonl): the clock holds at ~1.2 GHz under that load"},
                    "flop_model": model + "; rays = segments (the active lanes) on the matrix cores",
                    "valu_algorithmic": {"achieved": round(flops, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                                         "frac": round(flops / VALU_PEAK_TFLOPS, 4),
