@@ -701,6 +701,9 @@ const Variant kVariants[] = {
     RT2_VARIANT(234, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4; x.serial = 1; return x; }()>, 256, "mfma/256/k5/notn/coop8/w4/imax/minred/ymma/t12/llds2/ser1/cmp"),
     RT2_VARIANT(235, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4; x.serial = 3; return x; }()>, 256, "mfma/256/k5/notn/coop8/w4/imax/minred/ymma/t12/llds2/ser3/cmp"),
     RT2_VARIANT(236, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4; x.compact = false; return x; }()>, 256, "mfma/256/k5/notn/coop8/w4/imax/minred/ymma/t12/llds2/ser4"),
+    RT2_VARIANT(240, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4; x.tail_lanes = 4; return x; }()>, 256, "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
+    RT2_VARIANT(241, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4; x.tail_lanes = 16; return x; }()>, 256, "mfma/256/k5/notn/coop16/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
+    RT2_VARIANT(242, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4; x.tail_lanes = 0; return x; }()>, 256, "mfma/256/k5/notn/coop0/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
     RT2_VARIANT(239, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4; x.diag = true; return x; }()>, 256, "mfma/256/k5/notn/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp/diag"),
     RT2_VARIANT(232, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTn; x.diag = true; return x; }()>, 256, "mfma/256/k5/notn/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp/diag"),
     RT2_VARIANT(229, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5; x.diag = true; return x; }()>, 256, "mfma/256/k5/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp/diag"),
