@@ -1,0 +1,294 @@
+// The 5-product matrix filter (rt2_mfma.h, MfmaSpec::k5) with its record
+// operands streamed through workgroup-shared LDS tiles: the north star's
+// "triangle arrays streamed from HBM in coalesced tiles and staged in LDS".
+// Included by rt2_render.hip only (one translation unit; internal linkage).
+//
+// What it replaces: in render_mfma every wave loads its own copy of each
+// 32-triangle group's records (4 operands x 1 KiB + tau + the m.z bound) from
+// L2/MALL — for a 100k-triangle scene 12.8 MB per wave-segment, about 2 B per
+// (ray, triangle) pair, half of it missing the L2 (DESIGN.md, config C PMC).
+// The reference reads `triangles[i]` from SSBO 1 in every leaf test
+// (compute.glsl:429-431, block :75-78).
+//
+// Here the NW waves of a workgroup (one workgroup per CU) sweep the same
+// records in the same order, so each tile of K groups is brought into LDS
+// once per workgroup and segment, by LDS-DMA (global_load_lds_dwordx4: 1-KiB
+// coalesced pieces, no VGPRs), split across the waves and double-buffered:
+// tile t+1 is in flight while tile t is swept.  One barrier per tile.  The
+// record traffic from L2 falls NW-fold.  The arithmetic of every product,
+// threshold and exact test is sweep_k16's 5-product form term for term, so
+// the result is the sequential strict `dst < best` scan's bit for bit.
+//
+// Register budget: the k16 tiled attempt (render_mfma_tiled) kept the path
+// state in VGPRs across the tile loop and spilled 45 of them; this kernel
+// parks it in LDS (the packed 15-word stash of the 4-wave build) in every
+// wave, sweeping or not, so that no path state is live across the loop.
+#pragma once
+
+namespace {
+
+// LDS of one workgroup's record tiles: 2 buffers x K groups x the 4 operands
+// the 5-product form reads (U0, V0, X0, T1: k16 ops 0, 2, 4, 6) as 64 lanes x
+// 16 B, the per-triangle scale tau and the m.z residual bound.
+template <int K>
+struct K5Tiles {
+    h8 rec[2][K * 4 * 64];
+    float tau[2][K * 32];
+    float2 bnd[2][K * 32];
+};
+
+__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Closest hit of every lane's ray over all triangles, or (sweeping = false)
+// only the workgroup's tile traffic and barriers: every wave of the workgroup
+// calls it in every segment the workgroup runs.  Returns false when the wave's
+// rays are outside the filter's range (nothing computed; wave-uniform).
+template <MfmaSpec S>
+__device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, MfmaK16PackedLds& sh, K5Tiles<S.tile_groups>& tl,
+                                               const f3& o, const f3& d, float& best, int& bi, float& bestK,
+                                               MfmaDiag& dg, bool sweeping, bool upper) {
+    static_assert(S.k5 && S.ymma && S.imax && S.minred && S.tile_groups > 0, "the 5-product form");
+    constexpr int K = S.tile_groups, NW = S.block / 64;
+    const int lane = (int)lane_id();
+    const int r32 = lane & 31, hl = lane >> 5, wave = (int)(threadIdx.x >> 6);
+    MfmaScale sc{0.0f, 0.0f, 0.0f};
+    float zlo = 0.0f, zhi = 0.0f;
+    h8 a0[2], a1[2], y1[2];
+    bool compute = false, in_range = true;
+    auto write_y = [&](float bkv) {
+        _Float16 s[16];
+        mfma_y_chunk(s, d, o, bkv, sc.sigma, sc.Bmax);
+        h8* row = reinterpret_cast<h8*>(&sh.ray[lane][32]);
+        row[0] = h8{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7]};
+        row[1] = h8{s[8], s[9], s[10], s[11], s[12], s[13], s[14], s[15]};
+    };
+    auto read_y = [&]() {
+#pragma unroll
+        for (int R = 0; R < 2; R++) y1[R] = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][32 + 8 * hl]);
+    };
+    if (sweeping) {
+        const f3 m = cross(d, o);
+        in_range = mfma_scale<S>(p.mfma_A, o, d, m, sc);
+        if (in_range) {
+            mfma_main_row(&sh.ray[lane][0], d, m, o, sc.sigma);
+            // the wave's largest |ray lo| and |ray hi| of m.z (sweep_k16's k5 bound)
+            const float vz = m.z * sc.sigma;
+            const _Float16 hz = (_Float16)vz;
+            const _Float16 lz = (_Float16)(vz - (float)hz);
+            zhi = wave_max(fabsf((float)hz));
+            zlo = wave_max(fabsf((float)lz));
+            write_y(bestK);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int R = 0; R < 2; R++) {
+                a0[R] = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][8 * hl]);
+                if constexpr (!S.no_tn) a1[R] = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][16 + 8 * hl]);
+            }
+            read_y();
+            compute = true;
+        }
+    }
+    const int ng = (p.n_tris + 31) >> 5, nt = (ng + K - 1) / K;
+    const h8* gsrc = reinterpret_cast<const h8*>(p.mfma_k16_frag);
+    // LDS-DMA of tile t into buffer t & 1, round-robin over the waves: 4 record
+    // pieces per group (1 KiB each: a lane's 16 B land at base + 16 lane),
+    // then the groups' bounds (256 B per group) and scales (128 B per group)
+    // as 16-B pieces with the lanes past the tile's end masked off
+    auto issue = [&](int t) {
+        const int g0 = t * K, gn = min(K, ng - g0);
+        const int nrec = gn * 4, nbnd = (gn * 16 + 63) / 64, ntau = (gn * 8 + 63) / 64;
+        const int b = t & 1;
+        for (int pc = wave; pc < nrec + nbnd + ntau; pc += NW) {
+            if (pc < nrec) {
+                const int gi = pc >> 2, op = 2 * (pc & 3);
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(gsrc + ((size_t)(g0 + gi) * kK16Ops + op) * 64 + lane),
+                    (__attribute__((address_space(3))) void*)&tl.rec[b][pc * 64], 16, 0, 0);
+            } else if (pc < nrec + nbnd) {
+                const int q = pc - nrec;
+                if (64 * q + lane < gn * 16)
+                    __builtin_amdgcn_global_load_lds(
+                        (const __attribute__((address_space(1))) void*)(reinterpret_cast<const float4*>(
+                                                                            p.mfma_k16_bnd + 32 * (size_t)g0) +
+                                                                        64 * q + lane),
+                        (__attribute__((address_space(3))) void*)&tl.bnd[b][128 * q], 16, 0, 0);
+            } else {
+                const int q = pc - nrec - nbnd;
+                if (64 * q + lane < gn * 8)
+                    __builtin_amdgcn_global_load_lds(
+                        (const __attribute__((address_space(1))) void*)(reinterpret_cast<const float4*>(
+                                                                            p.mfma_k16_tau + 32 * (size_t)g0) +
+                                                                        64 * q + lane),
+                        (__attribute__((address_space(3))) void*)&tl.tau[b][256 * q], 16, 0, 0);
+            }
+        }
+    };
+    if (nt > 0) issue(0);
+    for (int t = 0; t < nt; t++) {
+        wait_vm0();       // this wave's pieces of tile t have landed
+        __syncthreads();  // every wave's have; every wave is done with buffer (t + 1) & 1 (tile t - 1)
+        if (t + 1 < nt) issue(t + 1);
+        if (!compute) continue;
+        const int b = t & 1, gn = min(K, ng - t * K);
+        for (int gi = 0; gi < gn; gi++) {
+            const int G = t * K + gi;
+            const h8* tb = &tl.rec[b][gi * 4 * 64 + lane];
+            const h8 b0 = tb[0], b2 = tb[64], b4 = tb[128], b6 = tb[192];
+            const float tau = tl.tau[b][gi * 32 + r32];
+            const float2 bnd = tl.bnd[b][gi * 32 + r32];
+            // sweep_k16's threshold: tau T + the bound of the left-out m.z
+            // slots, padded by 2^-10 for its own rounding ("The
+            // 5-product form")
+            const float Tl = tau * sc.Tw + (bnd.x * zlo + bnd.y * zhi) * 1.0009765625f;
+            int tmin = 0x7fffffff;
+#pragma unroll
+            for (int R = 0; R < 2; R++) {
+                if (R == 1 && !upper) break;
+                const f16v zero = {};
+                const f16v U = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[R], b0, zero, 0, 0, 0);
+                const f16v V = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[R], b2, zero, 0, 0, 0);
+                const f16v X = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[R], b4, zero, 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                int t3[16];
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    t3[i] = max(max(__float_as_int(U[i]), __float_as_int(V[i])), __float_as_int(X[i]));
+                __builtin_amdgcn_sched_barrier(0);
+                f16v T = {};
+                if constexpr (!S.no_tn) T = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[R], b6, zero, 0, 0, 0);
+                const f16v Y = __builtin_amdgcn_mfma_f32_32x32x16_f16(y1[R], b6, zero, 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int i = 0; i < 16; i++) {
+                    if constexpr (S.no_tn)
+                        tmin = min(tmin, max(t3[i], __float_as_int(Y[i])));
+                    else
+                        tmin = min(tmin, max(max(t3[i], __float_as_int(T[i])), __float_as_int(Y[i])));
+                }
+                if (R == 1) __builtin_amdgcn_sched_barrier(0);
+            }
+            const unsigned long long M = __ballot(tmin <= __float_as_int(Tl));
+            if constexpr (S.diag) dg.groups += 1;
+            if (M) {
+                if constexpr (S.diag) dg.hot += 1;
+                // triangles of the group with a passing pair: the exact phase, in index order
+                uint32_t m32 = (uint32_t)(M | M >> 32);
+                const float bk0 = bestK;
+                while (m32) {
+                    const int tt = __builtin_ctz(m32);
+                    m32 &= m32 - 1;
+                    const int idx = 32 * G + tt;
+                    if (idx >= p.n_tris) break;
+                    if constexpr (S.diag) dg.exact += 1;
+                    cfloat* tp = (cfloat*)p.tri + 12 * idx;
+                    const MtQ qq = mt_quantities(o, d, ldc4(tp), ldc4(tp + 4), ldc4(tp + 8));
+                    if (mt_pass3(qq, bestK)) mt_exact(qq, idx, best, bi, bestK);
+                }
+                if (__ballot(bestK != bk0)) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();  // every lane has read the rows' previous Y slots
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    write_y(bestK);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    read_y();
+                }
+            }
+        }
+    }
+    return in_range;
+}
+
+// render_mfma's lockstep segment loop around sweep_k5_tiles: every wave of the
+// workgroup takes part in every tile barrier of every segment the workgroup
+// runs (block_any decides, workgroup-uniformly, whether it runs one), sweeping
+// only when it has rays and is not in the cooperative drain.  The path state
+// waits in LDS (lane_stash_packed) across the tile loop in every wave; the
+// launcher takes this kernel only when the packed fields hold the launch.
+template <MfmaSpec S>
+__global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves))) void render_mfma_k5t(RenderParams p_arg) {
+    static_assert(S.lane_lds == 2 && S.lockstep, "packed path state, lockstep segments");
+    constexpr int NW = S.block / 64;
+    __shared__ MfmaK16PackedLds wl[NW];
+    __shared__ K5Tiles<S.tile_groups> tl;
+    __shared__ BlockVote<NW> vote;
+    uint32_t vote_parity = 0;
+    MfmaK16PackedLds& sh = wl[threadIdx.x >> 6];
+    Lane L;
+    lane_init(L);
+    MfmaDiag dg;
+    for (;;) {
+        const RenderParams& p = kargs<RenderParams>();
+        advance(L, p);
+        unsigned long long act = __ballot(L.st == ST_TRACE);
+        if (!block_any<NW>(act != 0, vote, vote_parity)) break;
+        const bool coop = act != 0 && __popcll(act) <= (unsigned)S.tail_lanes && __any(L.st == ST_DONE);
+        const bool sweeping = act != 0 && !coop;
+        bool upper = true;
+        if constexpr (S.compact) {
+            if (sweeping && __popcll(act) <= 32) {
+                if (act >> 32) {
+                    const uint32_t l = lane_id(), nl = (uint32_t)__popcll(act);
+                    const bool live = (act >> l) & 1ull;
+                    const int to = 4 * (int)(live ? lanes_below(act) : nl + lanes_below(~act));
+                    lane_permute(L, to);
+                    act = __ballot(L.st == ST_TRACE);
+                }
+                upper = false;
+            }
+        }
+        const bool mine = L.st == ST_TRACE;
+        if (sweeping) {
+            // lanes without a ray carry the first live lane's (ST_DONE lanes
+            // never read their o, d again)
+            const int j0 = __builtin_ctzll(act);
+            const f3 o = mk(__shfl(L.o.x, j0), __shfl(L.o.y, j0), __shfl(L.o.z, j0));
+            const f3 dd = mk(__shfl(L.d.x, j0), __shfl(L.d.y, j0), __shfl(L.d.z, j0));
+            if (!mine) {
+                L.o = o;
+                L.d = dd;
+            }
+        }
+        const f3 ro = L.o, rd = L.d;
+        float best = 1e38f, bestK = 1e38f * 1.0009765625f;
+        int bi = -1;
+        lane_stash_packed(L, sh.lane, (int)lane_id());
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        const bool swept = sweep_k5_tiles<S>(p, sh, tl, ro, rd, best, bi, bestK, dg, sweeping, upper);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        lane_unstash_packed(L, sh.lane, (int)lane_id());
+        L.o = ro;
+        L.d = rd;
+        if (coop) {
+            float mybest = 1e38f;
+            int mybi = -1;
+            coop_each(act, L.o, L.d, p, mybest, mybi);
+            if (mine) {
+                L.bounce += 1;
+                L.segs += 1;
+                shade(L, p, mybest, mybi);
+            }
+            continue;
+        }
+        if (!act) continue;
+        if (!swept) coop_each(act, ro, rd, p, best, bi);
+        if (mine) {
+            L.bounce += 1;
+            L.segs += 1;
+            shade(L, p, best, bi);
+        }
+    }
+    const RenderParams& p = kargs<RenderParams>();
+    flush_counters(L, p);
+    if constexpr (S.diag)
+        if (lane_id() == 0) {
+            atomicAdd(p.seg_counter + 1, dg.groups);  // (wave, triangle group) sweeps
+            atomicAdd(p.seg_counter + 2, dg.hot);     // ... with a passing pair
+            atomicAdd(p.seg_counter + 3, dg.exact);   // (wave, triangle) exact tests
+        }
+}
+
+}  // namespace

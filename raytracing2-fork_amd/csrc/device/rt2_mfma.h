@@ -471,7 +471,7 @@ __device__ __forceinline__ void lane_stash(const Lane& L, uint32_t (*st)[64], in
                                     __float_as_uint(L.rayColor.z), __float_as_uint(L.incoming.x),
                                     __float_as_uint(L.incoming.y), __float_as_uint(L.incoming.z),
                                     __float_as_uint(L.colorCum.x), __float_as_uint(L.colorCum.y),
-                                    __float_as_uint(L.colorCum.z), L.segs, L.t0};
+                                    __float_as_uint(L.colorCum.z), L.segs, 0u};
 #pragma unroll
     for (int f = 0; f < kLaneStash; f++) st[f][l] = v[f];
 }
@@ -495,10 +495,9 @@ __device__ __forceinline__ void lane_permute(Lane& L, int to) {
     L.incoming = perm_f3(to, L.incoming);
     L.colorCum = perm_f3(to, L.colorCum);
     L.segs = (uint32_t)perm_i(to, (int)L.segs);
-    L.t0 = (uint32_t)perm_i(to, (int)L.t0);
 }
 // lane_lds = 2: 15 words (st:3 inside:1 bounce:12 ray:16 | item | x:16 y:16 |
-// frame | seed | colours | segs; t0 keeps its register); the launcher uses it
+// frame | seed | colours | segs); the launcher uses it
 // only when bounce <= 4095, rays per pixel <= 65535 and the image fits 16-bit
 // coordinates
 struct MfmaK16PackedLds {
@@ -546,7 +545,6 @@ __device__ __forceinline__ void lane_unstash(Lane& L, const uint32_t (*st)[64], 
     L.incoming = mk(__uint_as_float(st[12][l]), __uint_as_float(st[13][l]), __uint_as_float(st[14][l]));
     L.colorCum = mk(__uint_as_float(st[15][l]), __uint_as_float(st[16][l]), __uint_as_float(st[17][l]));
     L.segs = st[18][l];
-    L.t0 = st[19][l];
 }
 
 // bnd_out (the 5-product form, MfmaSpec::k5): per triangle, the largest
@@ -1297,16 +1295,40 @@ __global__ __launch_bounds__(64) void mfma_probe_kernel(RenderParams p, const fl
     }
 }
 
+// Closest hit of every ray of `act` (lane j's o, d), one ray at a time by the
+// whole wave (coop_closest: the sequential strict-< scan's result); lane j
+// receives its own ray's (best, bi), lanes outside `act` keep theirs.
+__device__ __forceinline__ void coop_each(unsigned long long act, const f3& o, const f3& d, const RenderParams& p,
+                                          float& best, int& bi) {
+    while (act) {
+        const int j = __builtin_ctzll(act);
+        act &= act - 1;
+        const f3 oj = mk(__shfl(o.x, j), __shfl(o.y, j), __shfl(o.z, j));
+        const f3 dj = mk(__shfl(d.x, j), __shfl(d.y, j), __shfl(d.z, j));
+        float b;
+        int bidx;
+        coop_closest(oj, dj, p.tri, p.n_tris, b, bidx);
+        if ((int)lane_id() == j) {
+            best = b;
+            bi = bidx;
+        }
+    }
+}
+
 // MFMA: render_smem's lockstep segment loop and cooperative drain with the
 // matrix-core filter (sweep_mfma) as the closest-hit sweep; a wave whose
-// rays leave the filter's range sweeps with the scalar-path filter instead.
+// rays leave the filter's range computes them with the cooperative drain's
+// code instead (coop_each).
 template <MfmaSpec S>
-__global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves))) void render_mfma(RenderParams p) {
+__global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves))) void render_mfma(RenderParams p_arg) {
+    const RenderParams& p = p_arg;
     using WL = std::conditional_t<
         S.k16, std::conditional_t<S.lane_lds == 2, MfmaK16PackedLds, std::conditional_t<S.lane_lds == 1, MfmaK16LaneLds, MfmaK16Lds>>,
         MfmaWaveLds>;
     __shared__ WL wl[S.block / 64];
     WL& sh = wl[threadIdx.x >> 6];
+    __shared__ BlockVote<S.block / 64> vote;  // lockstep: block_any
+    uint32_t vote_parity = 0;
     if constexpr (S.lds_pad > 0) {
         __shared__ uint32_t pad[S.lds_pad / 4];
         if (p.n_items == 0) pad[threadIdx.x] = 0;  // never taken at launch; keeps the allocation
@@ -1335,13 +1357,17 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
         }
     };
     for (;;) {
+        // the kernel arguments are re-read from the kernarg segment (scalar
+        // loads) in every segment instead of being held in SGPRs across the
+        // sweep (whose register pressure then spills them to VGPR lanes)
+        const RenderParams& p = kargs<RenderParams>();
         advance(L, p);
         unsigned long long act = __ballot(L.st == ST_TRACE);
         stamp(dg.t_advance);
         if constexpr (S.diag)
             if (p.wave_log && !wl_dry && __any(L.st == ST_DONE)) wl_dry = __builtin_amdgcn_s_memrealtime();
         if constexpr (S.lockstep) {
-            if (!__syncthreads_or(act != 0)) break;
+            if (!block_any<S.block / 64>(act != 0, vote, vote_parity)) break;
             if (!act) {
                 if constexpr (S.diag) wl_idle++;
                 continue;
@@ -1360,20 +1386,7 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
         if (__popcll(act) <= (unsigned)S.tail_lanes && __any(L.st == ST_DONE)) {
             float mybest = 1e38f;
             int mybi = -1;
-            unsigned long long mm = act;
-            while (mm) {
-                const int j = __builtin_ctzll(mm);
-                mm &= mm - 1;
-                const f3 oj = mk(__shfl(L.o.x, j), __shfl(L.o.y, j), __shfl(L.o.z, j));
-                const f3 dj = mk(__shfl(L.d.x, j), __shfl(L.d.y, j), __shfl(L.d.z, j));
-                float b;
-                int bidx;
-                coop_closest(oj, dj, p.tri, p.n_tris, b, bidx);
-                if ((int)lane_id() == j) {
-                    mybest = b;
-                    mybi = bidx;
-                }
-            }
+            coop_each(act, L.o, L.d, p, mybest, mybi);
             if (L.st == ST_TRACE) {
                 L.bounce += 1;
                 L.segs += 1;
@@ -1398,12 +1411,19 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
                 upper = false;
             }
         }
-        // lanes without a ray carry the first live lane's (their passes add no triangle)
+        // lanes without a ray carry the first live lane's (their passes add no
+        // triangle; such a lane is ST_DONE and never reads its o, d again)
         const int j0 = __builtin_ctzll(act);
         const bool mine = L.st == ST_TRACE;
-        const f3 o = mk(__shfl(L.o.x, j0), __shfl(L.o.y, j0), __shfl(L.o.z, j0));
-        const f3 dd = mk(__shfl(L.d.x, j0), __shfl(L.d.y, j0), __shfl(L.d.z, j0));
-        const f3 ro = mine ? L.o : o, rd = mine ? L.d : dd;
+        {
+            const f3 o = mk(__shfl(L.o.x, j0), __shfl(L.o.y, j0), __shfl(L.o.z, j0));
+            const f3 dd = mk(__shfl(L.d.x, j0), __shfl(L.d.y, j0), __shfl(L.d.z, j0));
+            if (!mine) {
+                L.o = o;
+                L.d = dd;
+            }
+        }
+        const f3 ro = L.o, rd = L.d;
         float best = 1e38f, bestK = 1e38f * 1.0009765625f;
         int bi = -1;
         bool swept;
@@ -1414,12 +1434,8 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 swept = sweep_k16<S>(p, sh, ro, rd, best, bi, bestK, dg, upper);
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                const uint32_t t0 = L.t0;
                 lane_unstash_packed(L, sh.lane, (int)lane_id());
-                L.t0 = t0;
-                // ro, rd are this lane's own ray where it has one; a lane without
-                // a ray never reads its o, d again (advance leaves only TRACE or DONE)
-                L.o = ro;
+                L.o = ro;  // (the same values: the stash does not hold o, d)
                 L.d = rd;
             } else {
                 lane_stash(L, sh.lane, (int)lane_id());
@@ -1435,8 +1451,10 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
             swept = sweep_k16<S>(p, sh, ro, rd, best, bi, bestK, dg, upper);
         else
             swept = sweep_mfma<S>(p, sh, ro, rd, best, bi, bestK, dg);
-        if (!swept && mine)
-            sweep_masked<8, true, Filter::Max3>(ro, rd, nullptr, (const float*)p.tri, p.n_tris, 0, best, bi, bestK);
+        // a ray outside the filter's range (wave-uniform): the wave computes each
+        // live ray's closest hit together (the drain's code, vector loads: no
+        // SGPR block of records competing with the sweep's registers)
+        if (!swept) coop_each(act, ro, rd, p, best, bi);
         stamp(dg.t_sweep);
         if (mine) {
             L.bounce += 1;

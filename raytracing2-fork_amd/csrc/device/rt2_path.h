@@ -19,7 +19,6 @@ struct Lane {
     bool inside;
     f3 o, d, rayColor, incoming, colorCum;
     uint32_t segs;
-    uint32_t t0;  // item start (s_memtime low bits), for the cost map
 };
 
 // S > 1: split mode (render_split) — the S waves of a workgroup hold the same
@@ -78,13 +77,16 @@ __device__ __forceinline__ void advance(Lane& L, const RenderParams& p) {
                     // frame_split: item = frame * n_pix + pixel (frame-major), so the
                     // last items of a launch are single pixel-frames
                     // n_items < 2^32 (checked on the host): 32-bit arithmetic
-                    const uint32_t it32 = (uint32_t)it, np32 = (uint32_t)p.n_pix;
+                    const uint32_t it32 = (uint32_t)it, np32 = opaque((uint32_t)p.n_pix);
                     const uint32_t f = p.frame_split ? it32 / np32 : 0u;
                     L.item = it32 - f * np32;
                     if (p.order && L.item < p.n_runs * 64u) L.item = p.order[L.item >> 6] * 64u + (L.item & 63u);
-                    L.t0 = (uint32_t)__builtin_amdgcn_s_memtime();
-                    int lr = (int)(L.item / (uint32_t)p.W);
-                    L.x = (int)(L.item - (uint32_t)lr * (uint32_t)p.W);
+                    // cost map (opt-in): the item's start clock waits in its own
+                    // slot (no register of the lane carries it)
+                    if (p.cost_out && split_writer<S>()) p.cost_out[L.item] = (uint32_t)__builtin_amdgcn_s_memtime();
+                    const uint32_t W = opaque((uint32_t)p.W);
+                    int lr = (int)(L.item / W);
+                    L.x = (int)(L.item - (uint32_t)lr * W);
                     L.y = shard_row(lr, p.tile_rows, p.rank, p.nranks);
                     L.frame = f;
                     L.st = ST_NEW_FRAME;
@@ -140,7 +142,7 @@ __device__ __forceinline__ void end_path(Lane& L, const RenderParams& p) {
     const bool writer = split_writer<S>();
     if (p.frame_split) {  // frame_accumulate adds the frames in order afterwards
         if (writer) p.frame_buf[(size_t)L.frame * p.n_pix + L.item] = make_float4(c.x, c.y, c.z, 0.0f);
-        if (writer && p.cost_out) p.cost_out[L.item] = (uint32_t)__builtin_amdgcn_s_memtime() - L.t0;
+        if (writer && p.cost_out) p.cost_out[L.item] = (uint32_t)__builtin_amdgcn_s_memtime() - p.cost_out[L.item];
         L.st = ST_NEED_ITEM;
         return;
     }
@@ -159,7 +161,7 @@ __device__ __forceinline__ void end_path(Lane& L, const RenderParams& p) {
     L.frame += 1;
     L.st = L.frame < p.frame_count ? ST_NEW_FRAME : ST_NEED_ITEM;
     if (L.st == ST_NEED_ITEM && writer && p.cost_out)
-        p.cost_out[L.item] = (uint32_t)__builtin_amdgcn_s_memtime() - L.t0;
+        p.cost_out[L.item] = (uint32_t)__builtin_amdgcn_s_memtime() - p.cost_out[L.item];
 }
 
 // texture(sampler2D, uv) with GL_LINEAR (no mipmaps) + GL_REPEAT, GL 4.3
@@ -303,7 +305,6 @@ __device__ __forceinline__ void lane_init(Lane& L) {
     L.inside = false;
     L.o = L.d = L.rayColor = L.incoming = L.colorCum = mk(0.0f, 0.0f, 0.0f);
     L.segs = 0;
-    L.t0 = 0;
 }
 
 template <int S = 1>

@@ -38,6 +38,7 @@ using namespace rt2d;
 #include "rt2_path.h"
 #include "rt2_brute.h"
 #include "rt2_mfma.h"
+#include "rt2_k5_tiles.h"
 #ifdef RT2_EXPERIMENTS
 #include "rt2_mfma32.h"
 #endif
@@ -578,6 +579,26 @@ constexpr MfmaSpec kMfmaK5NoTnW4 = [] {
     x.no_tn = true;
     return x;
 }();
+// the small-scene kernel (233) with the cooperative drain at <= 4 live rays
+// instead of 8 (config B 189.5 vs 194.4 ms, 1/8 slab 29.0 vs 29.4 ms;
+// profiles/r03_coop_ab_configB.json, r03_coop_shard_probe_configB.jsonl)
+constexpr MfmaSpec kMfmaK5NoTnW4C4 = [] {
+    MfmaSpec x = kMfmaK5NoTnW4;
+    x.tail_lanes = 4;
+    return x;
+}();
+// the 5-product form with workgroup-shared LDS record tiles (rt2_k5_tiles.h):
+// 12 waves (3 per SIMD, one workgroup per CU), K = 4 groups per tile
+constexpr MfmaSpec k5_tiles_spec(int K, bool no_tn, int tail, bool diag = false) {
+    MfmaSpec x = kMfmaK5W4;
+    x.block = 768;
+    x.waves = 3;
+    x.tile_groups = K;
+    x.no_tn = no_tn;
+    x.tail_lanes = tail;
+    x.diag = diag;
+    return x;
+}
 constexpr Bvh3Spec kBvhDefault{.block = 256, .thresh = 16, .slab = Slab::Markstein, .waves = 5, .diag = false};
 
 #ifdef RT2_EXPERIMENTS
@@ -646,7 +667,14 @@ const Variant kVariants[] = {
     // or 3 when the packed fields do not hold the image / rays / bounces
     RT2_VARIANT(233, K_MFMA, render_mfma<kMfmaK5NoTnW4>, 256, "mfma/256/k5/notn/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
     RT2_VARIANT(231, K_MFMA, render_mfma<kMfmaK5NoTn>, 256, "mfma/256/k5/notn/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"),
+    RT2_VARIANT(243, K_MFMA, render_mfma<kMfmaK5NoTnW4C4>, 256, "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
+    // LDS record tiles shared by the workgroup (rt2_k5_tiles.h; DESIGN.md "LDS record tiles")
+    RT2_VARIANT(250, K_MFMA, render_mfma_k5t<k5_tiles_spec(4, false, 0)>, 768, "mfmat5/768/k5/tile4/coop0/w3/llds2/cmp"),
+    RT2_VARIANT(252, K_MFMA, render_mfma_k5t<k5_tiles_spec(4, true, 0)>, 768, "mfmat5/768/k5/notn/tile4/coop0/w3/llds2/cmp"),
 #ifdef RT2_EXPERIMENTS
+    RT2_VARIANT(251, K_MFMA, render_mfma_k5t<k5_tiles_spec(4, false, 0, true)>, 768, "mfmat5/768/k5/tile4/coop0/w3/llds2/cmp/diag"),
+    RT2_VARIANT(253, K_MFMA, render_mfma_k5t<k5_tiles_spec(2, false, 0)>, 768, "mfmat5/768/k5/tile2/coop0/w3/llds2/cmp"),
+    RT2_VARIANT(254, K_MFMA, render_mfma_k5t<k5_tiles_spec(4, false, 8)>, 768, "mfmat5/768/k5/tile4/coop8/w3/llds2/cmp"),
     RT2_VARIANT(160, K_MFMA, render_mfma<k16_spec(3)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12"),
     RT2_VARIANT(161, K_MFMA, render_mfma<k16_spec(4)>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12"),
     RT2_VARIANT(162, K_MFMA, render_mfma<k16_spec(2)>, 256, "mfma/256/k16/coop8/w2/imax/minred/ymma/t12"),
@@ -1044,6 +1072,10 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     if (VP && ((s->traversal == RT2_TRAVERSAL_BVH) != is_bvh(VP->kind))) VP = nullptr;
     if (VP && VP->kind == K_RESIDENT && !fits) VP = nullptr;  // cannot hold this scene
     if (VP && (VP->kind == K_MFMA || VP->kind == K_MASSIST) && !s->mfma_ok) VP = nullptr;  // scene outside the filter's range
+    // the packed path state (lane_lds = 2) holds 16-bit x, y, rays per pixel and 12-bit bounce counts
+    const bool packed = u->width <= 65535 && u->height <= 65535 && u->maxBounceCount <= 4095 &&
+                        u->numRaysPerPixel <= 65535;
+    if (VP && !packed && std::strstr(VP->name, "llds2")) VP = nullptr;
     if (!VP && s->traversal == RT2_TRAVERSAL_BVH) VP = find_variant(kDefaultBvh);
     if (!VP) {
         int vi = s->n_tris <= kSmemMaxTris ? kDefaultBrute : kLargeScene;
@@ -1063,11 +1095,7 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
             // At config C's 100k triangles the fourth wave costs more than its
             // lanes gain (a 480x270x2 sample, 1.3 items per lane: 3.13 vs
             // 2.13 s for the k16 sweep)
-            if (s->n_tris <= kMfmaSlabMaxTris) {
-                const bool packed = u->width <= 65535 && u->height <= 65535 && u->maxBounceCount <= 4095 &&
-                                    u->numRaysPerPixel <= 65535;
-                vi = packed && find_variant(kMfmaSmall) ? kMfmaSmall : kMfmaSmallW3;
-            }
+            if (s->n_tris <= kMfmaSlabMaxTris) vi = packed && find_variant(kMfmaSmall) ? kMfmaSmall : kMfmaSmallW3;
         } else if (vi == kDefaultBrute) {
             // scenes outside the matrix filter's range (mfma_ok = 0):
             // items per resident lane decide the tail: a lane ends on a whole

@@ -83,7 +83,50 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// x as a value the compiler cannot treat as loop-invariant (an empty asm in
+// the loop): what is derived from it — the reciprocal sequence of an integer
+// division by a kernel argument — is recomputed where it is used, instead of
+// being hoisted out of a persistent loop and held in VGPRs across the sweep
+__device__ __forceinline__ uint32_t opaque(uint32_t x) {
+    asm volatile("" : "+s"(x));
+    return x;
+}
+
+// The kernel's first argument in the kernarg segment, through a pointer the
+// compiler cannot treat as loop-invariant: its fields are loaded (s_load from
+// the constant address space) where they are used.
+template <class T>
+__device__ __forceinline__ const T& kargs() {
+    typedef const __attribute__((address_space(4))) T CT;
+    CT* k = (CT*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(k));
+    return *(const T*)k;
+}
+
+// __syncthreads_or for a workgroup of NW waves: one vote word per wave in LDS,
+// one barrier (HIP's version reduces over a linear thread id that needs
+// threadIdx.y/z in registers for the whole kernel, and takes three barriers).
+// The votes are double-buffered by `parity` (wave-uniform, flipped per call):
+// a wave writes the other buffer next time, and it can only get there after
+// every wave has passed the next barrier, i.e. has read this one.
+template <int NW>
+struct BlockVote {
+    uint32_t v[2][NW];
+};
+template <int NW>
+__device__ __forceinline__ bool block_any(bool pred, BlockVote<NW>& bv, uint32_t& parity) {
+    const uint32_t mine = __ballot(pred) != 0ull;
+    if (lane_id() == 0) bv.v[parity][threadIdx.x >> 6] = mine;
+    __syncthreads();
+    uint32_t r = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) r |= bv.v[parity][w];
+    parity ^= 1u;
+    return r != 0;
+}
+
 __device__ __forceinline__ int shard_row(int local_row, int tile_rows, int rank, int nranks) {
+    tile_rows = (int)opaque((uint32_t)tile_rows);
     int t = local_row / tile_rows;
     return (t * nranks + rank) * tile_rows + local_row % tile_rows;
 }
