@@ -2,7 +2,7 @@
 """Benchmark of the MI355X render path on BASELINE.json's metric.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config B] [--traversal brute|bvh]
-                    [--no-cpu-baseline] [--no-alt] [--no-config-c]
+                    [--no-cpu-baseline] [--no-alt] [--no-config-c] [--no-config-e] [--no-scalar]
 
 --gpus N > 1 without a launcher starts N ranks itself (torch.distributed.run,
 one process per GPU, master 127.0.0.1); under a launcher WORLD_SIZE must equal N.
@@ -34,6 +34,10 @@ Prints ONE JSON line (rank 0):
                 (100k triangles, 1920x1080, 256 spp): one brute-force step with
                 its own roofline, the BVH kernel, the CPU baseline, parity, and
                 whether the >= 10x target is met and by which kernel
+  config_E      (1 GPU, config B runs) 1M triangles, mirror box, 16 bounces, 4
+                spp: the same legs as config_C
+  scalar_valu   (1 GPU) the no-MFMA scalar-path kernel (render_smem) on the
+                headline workload with its FP32-VALU roofline and parity
 """
 import argparse
 import glob
@@ -62,6 +66,7 @@ MFMA_FLOP_PER_PAIR = 320   # render_mfma 16x16x32 form: 5 quantities x 32 k-slot
 MFMA_K16_FLOP_PER_PAIR = 256  # the k16 sweep: 8 v_mfma_f32_32x32x16_f16 (32x32x16x2 FLOP each) per 1,024 pairs
 MFMA_K5_FLOP_PER_PAIR = 160   # its 5-product form (MfmaSpec::k5): 5 v_mfma_f32_32x32x16_f16 per 1,024 pairs
 MFMA_K5_NOTN_FLOP_PER_PAIR = 128  # ... without the -tn term (small scenes): 4 per 1,024 pairs
+SCALAR_VARIANT = 136       # render_smem forced (rt2_render.hip): the no-MFMA scalar-path kernel
 TARGET_RATIO = 10.0        # north star: >= 10x the CPU reference at config C on 1 GPU
 KERNEL_FILES = {"mfma": "render_mfma", "massist": "render_assist", "smem": "render_smem", "split": "render_split", "tiled": "render_tiled", "assist": "render_assist",
                 "resident": "render_resident", "bvh4": "render_bvh4", "bvh3": "render_bvh3", "bvh2": "render_bvh2",
@@ -81,6 +86,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-alt", action="store_true", help="skip timing the other traversal beside the headline")
     ap.add_argument("--no-config-c", action="store_true", help="skip the config C (north-star target) leg")
+    ap.add_argument("--no-config-e", action="store_true", help="skip the config E (1M triangles, mirror box) leg")
+    ap.add_argument("--no-scalar", action="store_true",
+                    help="skip the scalar-VALU leg (render_smem, the north star's no-MFMA kernel, on the headline workload)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target seconds per CPU baseline mode")
     ap.add_argument("--plumbing", action="store_true",
                     help="launch/collective path only, no GPU (CPU tests of --gpus N): each rank gathers a synthetic "
@@ -372,19 +380,22 @@ def cpu_summary(res, threads, host, sample_desc, gpu_values):
     return out
 
 
-def config_c_leg(torch, rt2, stream, threads, host, seconds, do_cpu):
-    """The north-star target configuration on one GPU: brute force (1 timed
-    step: ~1.5 min of kernel) with its roofline, the BVH traversal (3 steps),
+def config_leg(torch, rt2, stream, threads, host, seconds, do_cpu, name="C"):
+    """A second configuration on one GPU, timed beside the headline: config C
+    (the north-star target: 100k triangles, 256 spp) or config E (1M
+    triangles, mirror box, 16 bounces: the divergence stress).  Brute force (1
+    timed step: ~33 s / ~12 s of kernel) with its roofline (PMC traffic from
+    profiles/pmc_config<X>.json when it matches), the BVH traversal (3 steps),
     the CPU baseline on the same sample and parity against the oracle."""
     import numpy as np
-    sd, spec = rt2.build_config_scene("C")
+    sd, spec = rt2.build_config_scene(name)
     u = rt2.offline_uniforms(spec.width, spec.height, spec.bounces, spec.rays, sd.num_triangles)
     scene = rt2.Scene(sd, torch.cuda.current_device())
     sh = rt2.shard()
     accum = torch.zeros((spec.height, spec.width, 4), dtype=torch.float32, device="cuda")
     image = torch.empty_like(accum)
     samples = spec.width * spec.height * spec.rays * spec.frames
-    out = {"workload": f"config C: {spec.description}", "width": spec.width, "height": spec.height,
+    out = {"workload": f"config {name}: {spec.description}", "width": spec.width, "height": spec.height,
            "rays_per_pixel": spec.rays, "frames": spec.frames, "max_bounce": spec.bounces,
            "triangles": sd.num_triangles}
     legs, imgs = {}, {}
@@ -398,7 +409,7 @@ def config_c_leg(torch, rt2, stream, threads, host, seconds, do_cpu):
         rf = roofline(st.tests / steps, st.node_visits / steps, kern_ms, st.segments / steps, sd.num_triangles,
                       variant)
         rf["kernel"] = kernel_label(variant)
-        attach_traffic(rf, "C" if trav == "brute" else "C_bvh", variant, kern_ms)
+        attach_traffic(rf, name if trav == "brute" else f"{name}_bvh", variant, kern_ms)
         legs[trav] = {"value": round(samples * steps / el / 1e6, 4), "unit": "Msamples/s", "steps": steps,
                       "ms_per_step": round(el / steps * 1e3, 1), "roofline": rf,
                       "segments_per_sample": round(st.segments / (samples * steps), 4)}
@@ -409,11 +420,13 @@ def config_c_leg(torch, rt2, stream, threads, host, seconds, do_cpu):
     if do_cpu:
         res, parity = cpu_baseline(sd, spec, u, imgs, threads, seconds)
         desc = (f"{res['bvh']['pixels']} of {spec.width * spec.height} pixels (BVH mode; brute mode "
-                f"{res['brute']['pixels']}), evenly spread in raster order, full 256 spp, "
+                f"{res['brute']['pixels']}), evenly spread in raster order, full {spec.rays * spec.frames} spp, "
                 f"{res['bvh']['seconds']:.1f} s")
         cb = cpu_summary(res, threads, host, desc, {"brute": legs["brute"]["value"], "bvh": legs["bvh"]["value"]})
         out["cpu_baseline"] = cb
         out["parity"] = parity
+        if name != "C":
+            return out
         tgt = {"target": f">= {TARGET_RATIO:g}x the CPU reference's Msamples/s at config C on 1 GPU",
                "cpu_reference": f"oracle/ BVH traversal (the reference's algorithm) on {threads} CPUs",
                "brute_ratio": cb["gpu_brute_over_cpu_bvh"], "bvh_ratio": cb["gpu_bvh_over_cpu_bvh"],
@@ -583,6 +596,29 @@ def main():
             "note": "brute force and the reference BVH traversal agree except on exact distance ties"}
         scene.set_traversal(args.traversal)
         scene.set_variant(args.variant)
+    if world == 1 and args.traversal == "brute" and not args.no_scalar and sd.num_triangles <= 20000:
+        # the north star's literal kernel: one work-item per pixel-sample, the
+        # reference's 53-FLOP Moller-Trumbore per pair on the FP32 VALU, no
+        # MFMA (render_smem forced) — its VALU roofline is the physical one
+        # for that kernel; same workload, same bracket, never `value`
+        img_main = img.clone()
+        scene.set_variant(SCALAR_VARIANT)
+        renderer.accum.zero_()
+        scene.render(u, 0, spec.frames, renderer.sh, renderer.accum.data_ptr(), 0, stream.cuda_stream)
+        nsteps = max(1, min(args.steps, 2))
+        el3, km3, st3 = timed_renders(torch, rt2, scene, u, spec.frames, renderer.sh, renderer.accum,
+                                      renderer.image, nsteps, stream)
+        v3 = launched_variant(rt2, scene)
+        rf3 = roofline(st3.tests / nsteps, 0, km3, st3.segments / nsteps, sd.num_triangles, v3)
+        rf3["kernel"] = kernel_label(v3)
+        attach_traffic(rf3, f"{spec.name}_scalar", v3, km3)
+        out["scalar_valu"] = {
+            "value": round(samples_per_step * nsteps / el3 / 1e6, 3), "unit": "Msamples/s", "steps": nsteps,
+            "ms_per_step": round(el3 / nsteps * 1e3, 3), "roofline": rf3,
+            "pixels_differing_from_main": int((renderer.image[..., :3] != img_main[..., :3]).any(-1).sum().item()),
+            "note": "render_smem (variant 136): scalar-cache triangle records, the exact filtered test on the VALU, "
+                    "no MFMA; bit-identical to the headline kernel"}
+        scene.set_variant(args.variant)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test infrastructure: the CPU baseline and the parity checker only
     threads, host = oracle.default_threads(), oracle.host_cpu_info()
@@ -593,11 +629,14 @@ def main():
                 f"reference BVH traversal (compute.glsl:410-460), {res['bvh']['seconds']:.1f} s")
         out["cpu_baseline"] = cpu_summary(res, threads, host, desc, gpu_values)
         out["parity"] = parity
-    if world == 1 and spec.name == "B" and not args.no_config_c:
+    if world == 1 and spec.name == "B" and not (args.no_config_c and args.no_config_e):
         scene.close()
         torch.cuda.empty_cache()
-        out["config_C"] = config_c_leg(torch, rt2, stream, threads, host, args.cpu_seconds,
-                                       not args.no_cpu_baseline)
+        for name, skip in (("C", args.no_config_c), ("E", args.no_config_e)):
+            if not skip:
+                out[f"config_{name}"] = config_leg(torch, rt2, stream, threads, host, args.cpu_seconds,
+                                                   not args.no_cpu_baseline, name)
+                torch.cuda.empty_cache()
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -151,8 +151,10 @@ typedef struct rt2_scene rt2_scene;
 /* Replaces the three SSBO uploads (rayTracing.cpp:1323-1325, SSBO.cpp:3-10,
  * glBufferData GL_STATIC_DRAW: the arrays are copied, the caller keeps
  * ownership).  `nodes` may be NULL (brute-force traversal does not need it).
- * Materials with materialType TEXTURE sample nothing yet (numTextures = 0
- * semantics of compute.glsl:349-350: black attenuation). */
+ * Materials with materialType TEXTURE sample the images given to
+ * rt2_scene_set_textures (getTriangleTextureColor, compute.glsl:342-368);
+ * until that call they read black, as compute.glsl:349-350 does for a
+ * texture index outside numTextures. */
 int rt2_scene_create(const rt2_triangle* tris, int32_t n_tris,
                      const rt2_material* mats, int32_t n_mats,
                      const rt2_node* nodes, int32_t n_nodes,
@@ -213,6 +215,22 @@ int rt2_resolve_rgb8_reference(const uint32_t* accum8, int64_t n_pixels, uint32_
  * ranks (one process per GPU), rank r renders the rows of rt2_shard
  * {tile_rows, r, N} and ONE ncclGather (RCCL over xGMI) brings the resolved
  * slabs to the root, which un-interleaves them: bit-identical to one GPU.
+ *
+ * Failure contract (raytracing2-fork_amd/csrc/device/rt2_comm_protocol.h):
+ * every rank issues the same collectives in the same order.  A rank-local
+ * failure (arguments, a shard that does not match the communicator, device
+ * memory, a failed render) is decided by an agreement step — a 2-int
+ * ncclAllReduce(max) read back on the host — before any gather, so every
+ * rank returns < 0 and no gather is issued.  A rank that cannot take part in
+ * an agreement (its communicator was aborted, the agreement's own copy or
+ * allreduce fails) aborts and returns; its peers wait for it at most
+ * RT2_COMM_TIMEOUT_S seconds (default 600; every host wait on a collective is
+ * a poll of the stream and ncclCommGetAsyncError with that deadline), then
+ * abort their communicator and return < 0.  An aborted owned communicator is
+ * unusable: destroy it.  A wrapped communicator is never aborted here (its
+ * owner must abort it); the handle only refuses further use.
+ * RT2_FAULT_AT=<site>[@rank] injects a failure (tests only; sites
+ * gather.prepare, gather.issue, check, render, agree.copy).
  * ---------------------------------------------------------------------- */
 #define RT2_COMM_ID_BYTES 128 /* sizeof(ncclUniqueId) */
 typedef struct rt2_comm rt2_comm;
@@ -233,12 +251,12 @@ int rt2_comm_check(rt2_comm* comm);
  * 16-byte pixels (an rgba32f image or the uint32x4 8-bit sums), device memory —
  * to `root` with one ncclGather and un-interleaves it there into d_image
  * (height*width pixels, device; ignored on other ranks).  shard.rank/nranks
- * must be the communicator's.  Asynchronous on `stream`.  Every rank issues the
- * one ncclGather even when it fails locally (a root without d_image gathers
- * into scratch, then returns < 0); a local failure that cannot take part (out
- * of device memory, a shard that does not match the communicator) aborts an
- * owned communicator (ncclCommAbort: the peers' gather fails instead of
- * blocking; destroy it afterwards) — a wrapped one is left to its owner. */
+ * must be the communicator's.  The ranks first agree that each of them can
+ * take part (one agreement step on the communicator's own stream: the host
+ * waits for it, not for `stream`); the gather and the un-interleave are then
+ * asynchronous on `stream`.  A local failure (a root without d_image, a
+ * shard that does not match, no device memory) makes every rank return < 0
+ * with nothing issued. */
 int rt2_gather_slabs(rt2_comm* comm, const void* d_slab, int32_t width, int32_t height, rt2_shard shard,
                      int32_t root, void* d_image, void* stream);
 /* The root's un-interleave alone: d_gathered = [nranks][max_rows][width]
@@ -253,9 +271,10 @@ int rt2_unshard_slabs(const void* d_gathered, int32_t max_rows, int32_t width, i
  * ignored.  Blocking; every rank must call it.  The 8-bit sums are accumulated
  * and gathered when ANY rank passes out_rgb8 (so ranks may pass different
  * pointers), and the ranks agree before the gather that every one of them
- * rendered (two 2-int ncclAllReduce(max) steps): a rank-local failure makes
- * every rank return < 0 ("a peer rank failed") instead of leaving peers
- * blocked in the gather. */
+ * rendered (two agreement steps): a rank-local failure makes every rank
+ * return < 0 ("a peer rank failed") instead of leaving peers blocked in the
+ * gather.  The host waits for the gathers under the RT2_COMM_TIMEOUT_S
+ * deadline before the root copies the image out. */
 int rt2_render_host_gather(rt2_scene* scene, const rt2_uniforms* uniforms, uint32_t frame_begin,
                            uint32_t frame_count, rt2_shard shard, rt2_comm* comm, int32_t root,
                            float* out_rgba, uint8_t* out_rgb8);

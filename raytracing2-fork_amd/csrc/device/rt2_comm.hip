@@ -15,10 +15,14 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 
 #include "../../../include/rt2.h"
+#include "rt2_comm_protocol.h"
 
 namespace rt2h {
 void set_error(const std::string& msg);
@@ -110,7 +114,8 @@ struct rt2_comm {
     DevBuf hgathered;              // rt2_render_host_gather: root's [nranks][max_rows][W] (not shared with
                                    // rt2_gather_slabs, whose use may still be in flight on another stream)
     DevBuf image, image8, rgb8;    // rt2_render_host_gather: root's whole image
-    DevBuf status;                 // rt2_render_host_gather: the ranks' agreement words (int32 x 2)
+    DevBuf status;                 // the agreement words (int32 x 2) on the device
+    int32_t* hstatus = nullptr;    // ... and in pinned host memory (copies that never block the host)
 };
 
 extern "C" int rt2_comm_unique_id(uint8_t* id) {
@@ -132,37 +137,102 @@ static int comm_setup(rt2_comm* c) {
     c->rank = r;
     HIPCHECK(hipSetDevice(c->device));
     HIPCHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHECK(hipHostMalloc((void**)&c->hstatus, 2 * sizeof(int32_t), hipHostMallocDefault));
     return c->status.ensure(2 * sizeof(int32_t));  // allocated up front: the agreement step cannot fail on memory
 }
 
-// Every rank calls the same collectives in the same order, whatever happened
-// locally: a rank that returned early would leave its peers blocked in the
-// next collective.  agree_max is rt2_render_host_gather's agreement step (one
-// 2-int ncclAllReduce(max) on the communicator's stream, read back on the
-// host): v[0] = "this rank failed", v[1] = "this rank wants the 8-bit sums".
-static int agree_max(rt2_comm* c, int32_t v[2]) {
-    HIPCHECK(hipMemcpyAsync(c->status.p, v, 2 * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
-    NCCLCHECK(ncclAllReduce(c->status.p, c->status.p, 2, ncclInt32, ncclMax, c->comm, c->stream));
-    HIPCHECK(hipMemcpyAsync(v, c->status.p, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-    HIPCHECK(hipStreamSynchronize(c->stream));
-    return 0;
+namespace {
+
+// Deadline of every host wait on a collective (RT2_COMM_TIMEOUT_S, default
+// 600 s: the agreement after the render also waits for the slowest rank's
+// render).
+double comm_timeout_s() {
+    const char* e = std::getenv("RT2_COMM_TIMEOUT_S");
+    const double v = e && *e ? std::atof(e) : 0.0;
+    return v > 0.0 ? v : 600.0;
 }
 
-// A rank-local failure inside rt2_gather_slabs (asynchronous, so there is no
-// agreement step): an owned communicator is aborted so that the peers' gather
-// fails instead of blocking forever; it is unusable afterwards (destroy it).  A
-// wrapped communicator belongs to the caller and is left to the caller's abort.
-static int fail_collective(rt2_comm* c, const std::string& msg) {
-    if (c->owned && c->comm && !c->aborted) {
-        (void)ncclCommAbort(c->comm);
-        c->comm = nullptr;
-        c->aborted = true;
-        rt2h::set_error(msg + " (communicator aborted so that the peer ranks fail instead of blocking)");
-    } else {
-        rt2h::set_error(msg);
+// RCCL transport of the gather protocol (rt2_comm_protocol.h).  Fault
+// injection for the failure tests: RT2_FAULT_AT=<site>[@rank] makes this rank
+// (every rank without @rank) fail at that site — gather.prepare,
+// gather.issue, check, render (the protocol's sites) or agree.copy (this
+// transport's: the rank cannot take part in the agreement at all).
+struct RcclTransport {
+    rt2_comm* c;
+    bool usable() const { return c->comm && !c->aborted; }
+    bool fault(const char* site) const {
+        const char* e = std::getenv("RT2_FAULT_AT");
+        if (!e || !*e) return false;
+        const std::string f(e);
+        const size_t at = f.find('@');
+        if (f.substr(0, at) != site) return false;
+        return at == std::string::npos || std::atoi(f.c_str() + at + 1) == c->rank;
     }
-    return -1;
-}
+    // an owned communicator is aborted (ncclCommAbort); a wrapped one belongs to
+    // the caller, who has to abort it: this handle only refuses further use
+    void abort(const std::string& why) {
+        if (c->owned && c->comm && !c->aborted) {
+            (void)ncclCommAbort(c->comm);
+            c->comm = nullptr;
+        }
+        c->aborted = true;
+        rt2h::set_error("rt2 comm: " + why + (c->owned ? " (communicator aborted)" : " (abort the wrapped communicator)"));
+    }
+    // the host waits for stream `st` with a deadline: a collective whose peer
+    // never joins it is aborted there instead of blocking forever
+    int wait(hipStream_t st) {
+        const auto t0 = std::chrono::steady_clock::now();
+        const double limit = comm_timeout_s();
+        for (;;) {
+            const hipError_t q = hipStreamQuery(st);
+            if (q == hipSuccess) return 0;
+            if (q != hipErrorNotReady) {
+                abort(std::string("stream error while waiting for a collective: ") + hipGetErrorString(q));
+                return -1;
+            }
+            ncclResult_t a = ncclSuccess;
+            if (c->comm && ncclCommGetAsyncError(c->comm, &a) == ncclSuccess && a != ncclSuccess &&
+                a != ncclInProgress) {
+                abort(std::string("RCCL asynchronous error: ") + ncclGetErrorString(a));
+                return -1;
+            }
+            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
+                abort("a peer rank did not join the collective within RT2_COMM_TIMEOUT_S");
+                return -1;
+            }
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
+    }
+    // the agreement step: allreduce(max) of two ints on the communicator's own
+    // stream, read back into pinned memory and waited for under the deadline;
+    // any failure of this rank's part aborts
+    int agree(int32_t v[2]) {
+        if (!usable()) return -1;
+        c->hstatus[0] = v[0];
+        c->hstatus[1] = v[1];
+        if (fault("agree.copy") ||
+            hipMemcpyAsync(c->status.p, c->hstatus, 2 * sizeof(int32_t), hipMemcpyHostToDevice, c->stream) !=
+                hipSuccess) {
+            abort("the agreement's copy failed");
+            return -1;
+        }
+        if (ncclAllReduce(c->status.p, c->status.p, 2, ncclInt32, ncclMax, c->comm, c->stream) != ncclSuccess) {
+            abort("the agreement's allreduce could not be issued");
+            return -1;
+        }
+        if (hipMemcpyAsync(c->hstatus, c->status.p, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream) !=
+            hipSuccess) {
+            abort("the agreement's copy failed");
+            return -1;
+        }
+        if (wait(c->stream) != 0) return -1;
+        v[0] = c->hstatus[0];
+        v[1] = c->hstatus[1];
+        return 0;
+    }
+};
+
+}  // namespace
 
 extern "C" int rt2_comm_init(const uint8_t* id, int32_t nranks, int32_t rank, int32_t device, rt2_comm** out) {
     if (!id || !out || nranks < 1 || rank < 0 || rank >= nranks || device < 0) {
@@ -217,6 +287,7 @@ extern "C" void rt2_comm_destroy(rt2_comm* c) {
     for (DevBuf* b : {&c->send, &c->gathered, &c->acc, &c->res, &c->acc8, &c->hgathered, &c->image, &c->image8,
                       &c->rgb8, &c->status})
         b->release();
+    if (c->hstatus) (void)hipHostFree(c->hstatus);
     if (c->owned && c->comm) (void)ncclCommDestroy(c->comm);  // null after an abort
     delete c;
 }
@@ -273,41 +344,59 @@ extern "C" int rt2_gather_slabs(rt2_comm* c, const void* d_slab, int32_t width, 
         rt2h::set_error("rt2_gather_slabs: bad argument");
         return -1;
     }
-    if (rt2_comm_check(c) != 0) return -1;  // aborted, or a collective failed earlier on this communicator
-    if (sh.nranks != c->nranks || sh.rank != c->rank || rt2_shard_rows(height, sh) < 0)
-        return fail_collective(c, "rt2_gather_slabs: shard " + std::to_string(sh.rank) + "/" +
-                                      std::to_string(sh.nranks) + " does not match the communicator's rank " +
-                                      std::to_string(c->rank) + "/" + std::to_string(c->nranks));
-    if (!d_slab) return fail_collective(c, "rt2_gather_slabs: null slab");
     HIPCHECK(hipSetDevice(c->device));
     hipStream_t st = (hipStream_t)stream;
-    const int rows = rt2_shard_rows(height, sh), mr = max_slab_rows(height, sh);
-    const size_t slab_bytes = (size_t)mr * width * 16;
+    const bool is_root = c->rank == root;
+    int mr = 0;
+    size_t slab_bytes = 0;
     const void* send = d_slab;
-    if (rows < mr) {  // equal counts per rank: pad this slab to max_rows rows
-        if (c->send.ensure(slab_bytes) != 0) return fail_collective(c, "rt2_gather_slabs: out of device memory");
-        HIPCHECK(hipMemsetAsync(c->send.p, 0, slab_bytes, st));
-        HIPCHECK(hipMemcpyAsync(c->send.p, d_slab, (size_t)rows * width * 16, hipMemcpyDeviceToDevice, st));
-        send = c->send.p;
-    }
-    // a root without d_image still takes part (into the scratch buffer), then fails
-    const bool is_root = c->rank == root, root_ok = !is_root || d_image;
     void* recv = nullptr;
-    if (is_root) {
-        if (c->nranks == 1 && d_image) {
-            recv = d_image;  // the slab is the image
-        } else {
-            if (c->gathered.ensure(slab_bytes * c->nranks) != 0)
-                return fail_collective(c, "rt2_gather_slabs: out of device memory");
-            recv = c->gathered.p;
+    // this rank's checks, padding and receive buffer: a failure here is agreed
+    // on before the gather, so every rank returns < 0 and none issues it
+    auto prepare = [&](std::string& err) -> int {
+        if (sh.nranks != c->nranks || sh.rank != c->rank || rt2_shard_rows(height, sh) < 0) {
+            err = "shard " + std::to_string(sh.rank) + "/" + std::to_string(sh.nranks) +
+                  " does not match the communicator's rank " + std::to_string(c->rank) + "/" +
+                  std::to_string(c->nranks);
+            return -1;
         }
-    }
-    NCCLCHECK(ncclGather(send, recv, slab_bytes, ncclUint8, root, c->comm, st));
-    if (!root_ok) {
-        rt2h::set_error("rt2_gather_slabs: the root needs d_image");
+        if (!d_slab) return err = "null slab", -1;
+        if (is_root && !d_image) return err = "the root needs d_image", -1;
+        const int rows = rt2_shard_rows(height, sh);
+        mr = max_slab_rows(height, sh);
+        slab_bytes = (size_t)mr * width * 16;
+        if (rows < mr) {  // equal counts per rank: pad this slab to max_rows rows
+            if (c->send.ensure(slab_bytes) != 0) return err = "out of device memory", -1;
+            if (hipMemsetAsync(c->send.p, 0, slab_bytes, st) != hipSuccess ||
+                hipMemcpyAsync(c->send.p, d_slab, (size_t)rows * width * 16, hipMemcpyDeviceToDevice, st) !=
+                    hipSuccess)
+                return err = "the padding copy failed", -1;
+            send = c->send.p;
+        }
+        if (is_root) {
+            if (c->nranks == 1) {
+                recv = d_image;  // the slab is the image
+            } else {
+                if (c->gathered.ensure(slab_bytes * c->nranks) != 0) return err = "out of device memory", -1;
+                recv = c->gathered.p;
+            }
+        }
+        return 0;
+    };
+    auto gather = [&]() -> int {
+        return ncclGather(send, recv, slab_bytes, ncclUint8, root, c->comm, st) == ncclSuccess ? 0 : -1;
+    };
+    auto finish = [&](std::string& err) -> int {
+        if (is_root && c->nranks > 1 && rt2_unshard_slabs(c->gathered.p, mr, width, height, sh, d_image, st) != 0)
+            return err = rt2_last_error(), -1;
+        return 0;
+    };
+    RcclTransport t{c};
+    std::string err;
+    if (rt2p::gather_slabs(t, prepare, gather, finish, err) != 0) {
+        rt2h::set_error("rt2_gather_slabs: " + err);
         return -1;
     }
-    if (is_root && c->nranks > 1) return rt2_unshard_slabs(c->gathered.p, mr, width, height, sh, d_image, st);
     return 0;
 }
 
@@ -318,76 +407,74 @@ extern "C" int rt2_render_host_gather(rt2_scene* scene, const rt2_uniforms* u, u
         rt2h::set_error("rt2_render_host_gather: bad argument");
         return -1;
     }
-    if (rt2_comm_check(c) != 0) return -1;
     HIPCHECK(hipSetDevice(c->device));
     hipStream_t st = c->stream;
     const int H = (int)u->height, W = (int)u->width;
     const bool is_root = c->rank == root;
-    // Rank-local failures do not return before the agreement steps below: every
-    // rank issues the same collectives, then all fail together.
-    std::string err;
-    if (!scene || frame_count == 0 || W < 1 || H < 0)
-        err = "rt2_render_host_gather: bad argument";
-    else if (sh.nranks != c->nranks || sh.rank != c->rank || rt2_shard_rows(H, sh) < 0)
-        err = "rt2_render_host_gather: shard does not match the communicator";
-    // agreement 1: the 8-bit sums are accumulated and gathered when any rank
-    // asks for them (the root's out_rgb8 receives them), so the collective
-    // sequence never depends on one rank's pointers
-    int32_t v[2] = {err.empty() ? 0 : 1, out_rgb8 ? 1 : 0};
-    if (agree_max(c, v) != 0) return -1;
-    if (v[0]) {
-        rt2h::set_error(err.empty() ? "rt2_render_host_gather: a peer rank failed" : err);
-        return -1;
+    // Rank-local failures do not return before the agreement steps: every rank
+    // issues the same collectives, then all fail together (rt2_comm_protocol.h).
+    std::string aerr;
+    if (!scene || frame_count == 0 || W < 1 || H < 0) {
+        aerr = "bad argument";
+    } else if (sh.nranks != c->nranks || sh.rank != c->rank || rt2_shard_rows(H, sh) < 0) {
+        aerr = "shard does not match the communicator";
+    } else if (c->comm && !c->aborted) {
+        ncclResult_t a = ncclSuccess;
+        if (ncclCommGetAsyncError(c->comm, &a) != ncclSuccess || (a != ncclSuccess && a != ncclInProgress))
+            aerr = std::string("RCCL asynchronous error: ") + ncclGetErrorString(a);
     }
-    const bool rgb8 = v[1] != 0;
-    const int mr = max_slab_rows(H, sh);
-    const size_t slab = (size_t)mr * W * 16, whole = (size_t)W * H;
-    const int rows = rt2_shard_rows(H, sh);
-    auto local = [&]() -> int {
-        if (c->acc.ensure(slab) || c->res.ensure(slab) || (rgb8 && c->acc8.ensure(slab))) return -1;
-        if (is_root && (c->image.ensure(whole * 16) || (rgb8 && (c->image8.ensure(whole * 16) ||
-                                                                  c->rgb8.ensure(whole * 3)))))
-            return -1;
-        if (is_root && c->nranks > 1 && c->hgathered.ensure(slab * c->nranks)) return -1;
+    const int mr = aerr.empty() ? max_slab_rows(H, sh) : 0, rows = aerr.empty() ? rt2_shard_rows(H, sh) : 0;
+    const size_t slab = (size_t)mr * W * 16, whole = aerr.empty() ? (size_t)W * H : 0;
+    auto render = [&](bool rgb8, std::string& err) -> int {
+        if (c->acc.ensure(slab) || c->res.ensure(slab) || (rgb8 && c->acc8.ensure(slab)) ||
+            (is_root && (c->image.ensure(whole * 16) ||
+                         (rgb8 && (c->image8.ensure(whole * 16) || c->rgb8.ensure(whole * 3))))) ||
+            (is_root && c->nranks > 1 && c->hgathered.ensure(slab * c->nranks)))
+            return err = "out of device memory", -1;
         // slab buffers of max_rows rows, zeroed: the rows past this rank's slab
         // are the gather's padding
-        HIPCHECK(hipMemsetAsync(c->acc.p, 0, slab, st));
-        HIPCHECK(hipMemsetAsync(c->res.p, 0, slab, st));
-        if (rgb8) HIPCHECK(hipMemsetAsync(c->acc8.p, 0, slab, st));
-        if (rt2_render(scene, u, frame_begin, frame_count, sh, (float*)c->acc.p,
-                       rgb8 ? (uint32_t*)c->acc8.p : nullptr, st) != 0)
-            return -1;
-        if (rt2_resolve_rgba32f((const float*)c->acc.p, (int64_t)rows * W, frame_count, (float*)c->res.p, st) != 0)
-            return -1;
+        if (hipMemsetAsync(c->acc.p, 0, slab, st) != hipSuccess || hipMemsetAsync(c->res.p, 0, slab, st) != hipSuccess ||
+            (rgb8 && hipMemsetAsync(c->acc8.p, 0, slab, st) != hipSuccess))
+            return err = "hipMemsetAsync failed", -1;
+        if (rt2_render(scene, u, frame_begin, frame_count, sh, (float*)c->acc.p, rgb8 ? (uint32_t*)c->acc8.p : nullptr,
+                       st) != 0 ||
+            rt2_resolve_rgba32f((const float*)c->acc.p, (int64_t)rows * W, frame_count, (float*)c->res.p, st) != 0)
+            return err = rt2_last_error(), -1;
         return 0;
     };
-    // agreement 2: every rank rendered (errors on the stream surface at the
-    // agreement's synchronisation)
-    const int lrc = local();
-    const std::string lerr = lrc != 0 ? std::string(rt2_last_error()) : std::string();
-    v[0] = lrc != 0 ? 1 : 0;
-    v[1] = 0;
-    if (agree_max(c, v) != 0) return -1;
-    if (v[0]) {
-        rt2h::set_error(lrc != 0 ? lerr : std::string("rt2_render_host_gather: a peer rank failed"));
-        return -1;
-    }
-    void* recv = is_root ? (c->nranks == 1 ? c->image.p : c->hgathered.p) : nullptr;
-    NCCLCHECK(ncclGather(c->res.p, recv, slab, ncclUint8, root, c->comm, st));
-    if (is_root && c->nranks > 1 && rt2_unshard_slabs(c->hgathered.p, mr, W, H, sh, c->image.p, st) != 0) return -1;
-    if (rgb8) {
-        void* recv8 = is_root ? (c->nranks == 1 ? c->image8.p : c->hgathered.p) : nullptr;
-        NCCLCHECK(ncclGather(c->acc8.p, recv8, slab, ncclUint8, root, c->comm, st));
-        if (is_root && c->nranks > 1 && rt2_unshard_slabs(c->hgathered.p, mr, W, H, sh, c->image8.p, st) != 0)
+    auto gathers = [&](bool rgb8) -> int {
+        void* recv = is_root ? (c->nranks == 1 ? c->image.p : c->hgathered.p) : nullptr;
+        if (ncclGather(c->res.p, recv, slab, ncclUint8, root, c->comm, st) != ncclSuccess) return -1;
+        if (is_root && c->nranks > 1 && rt2_unshard_slabs(c->hgathered.p, mr, W, H, sh, c->image.p, st) != 0)
             return -1;
-        if (is_root && out_rgb8) {
+        if (rgb8) {
+            void* recv8 = is_root ? (c->nranks == 1 ? c->image8.p : c->hgathered.p) : nullptr;
+            if (ncclGather(c->acc8.p, recv8, slab, ncclUint8, root, c->comm, st) != ncclSuccess) return -1;
+            if (is_root && c->nranks > 1 && rt2_unshard_slabs(c->hgathered.p, mr, W, H, sh, c->image8.p, st) != 0)
+                return -1;
+        }
+        return 0;
+    };
+    RcclTransport t{c};
+    // the host waits for the whole sequence under the deadline (a peer that
+    // fails inside a gather cannot hang this rank), then the root copies out
+    auto finish = [&](bool rgb8, std::string& err) -> int {
+        if (is_root && rgb8 && out_rgb8) {
             hipLaunchKernelGGL(rgb8_kernel, dim3((unsigned)((whole + 255) / 256)), dim3(256), 0, st,
                                (const uint4*)c->image8.p, (long long)whole, (float)frame_count, (uint8_t*)c->rgb8.p);
-            HIPCHECK(hipGetLastError());
-            HIPCHECK(hipMemcpyAsync(out_rgb8, c->rgb8.p, whole * 3, hipMemcpyDeviceToHost, st));
+            if (hipGetLastError() != hipSuccess) return err = "the 8-bit resolve failed", -1;
         }
+        if (t.wait(st) != 0) return err = "waiting for the gathers failed", -1;
+        if (is_root && rgb8 && out_rgb8 && hipMemcpy(out_rgb8, c->rgb8.p, whole * 3, hipMemcpyDeviceToHost) != hipSuccess)
+            return err = "the copy of the 8-bit image failed", -1;
+        if (is_root && out_rgba && hipMemcpy(out_rgba, c->image.p, whole * 16, hipMemcpyDeviceToHost) != hipSuccess)
+            return err = "the copy of the image failed", -1;
+        return 0;
+    };
+    std::string err;
+    if (rt2p::render_gather(t, aerr.empty(), aerr, out_rgb8 != nullptr, render, gathers, finish, err) != 0) {
+        rt2h::set_error("rt2_render_host_gather: " + err);
+        return -1;
     }
-    if (is_root && out_rgba) HIPCHECK(hipMemcpyAsync(out_rgba, c->image.p, whole * 16, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipStreamSynchronize(st));
     return rt2_comm_check(c);
 }

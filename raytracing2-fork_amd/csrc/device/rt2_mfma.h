@@ -68,9 +68,8 @@ struct MfmaSpec {
     int serial = 0;         // k16: scheduling fences per 32-ray block: 1 = U V X products | their max | -tn Y
                             // products | the rest (48 accumulator VGPRs live); 2 = all 8 products | the reduction;
                             // 3 = 1 without the fence between the blocks; 4 = 3 without the fence at the group end
-    bool pipe = false;      // k16: software-pipelined sweep (sweep_k16_pipe): each 32-ray block's products are
-                            // interleaved with the previous block's reduction, the exact phase trails by one group
-    int tile_groups = 0;    // k16 (render_mfma_tiled): 32-triangle groups per LDS record tile shared by the workgroup
+    bool pipe = false;      // (removed: the software-pipelined k16 sweep, DESIGN.md "Tried and measured")
+    int tile_groups = 0;    // k5 (render_mfma_k5t, rt2_k5_tiles.h): 32-triangle groups per LDS record tile
     int sol = 0;            // speed-of-light probes (WRONG images; diag clocks only): 1 = every group reads group
                             // 0's records, 2 = no exact phase, 3 = 2 + only the U term is reduced; marginal-cost
                             // probes (same image): 4 = exact phase twice, 5 = products and reduction twice,
@@ -595,16 +594,11 @@ __device__ __forceinline__ K16Terms k16_terms(const h8& a0, const h8& a1, const 
 
 __device__ __forceinline__ f16v Y_unused_init() { return f16v{}; }
 template <MfmaSpec S, class SH>
-__device__ __forceinline__ bool sweep_k16_pipe(const RenderParams& p, SH& sh, const f3& o, const f3& d, float& best,
-                                               int& bi, float& bestK, MfmaDiag& dg);
-template <MfmaSpec S, class SH>
 __device__ __forceinline__ bool sweep_k16(const RenderParams& p, SH& sh, const f3& o, const f3& d, float& best,
                                           int& bi, float& bestK, MfmaDiag& dg, bool upper = true) {
     // upper = false: lanes 32..63 carry no ray of their own (MfmaSpec::compact moved the live rays to the
     // low half), so the second 32-ray block's products and reduction are skipped
     static_assert(S.ymma && S.imax && S.minred, "the k16 sweep implements the ymma / imax / minred form");
-    if constexpr (S.pipe)
-        if (upper) return sweep_k16_pipe<S>(p, sh, o, d, best, bi, bestK, dg);
     static_assert(!S.k5 || (!S.prefetch && !S.lateload && !S.afrag_lds && (S.serial == 1 || S.serial == 3 || S.serial == 4)),
                   "the 5-product form is built on the serialised sweep");
     const int lane = (int)lane_id();
@@ -858,327 +852,6 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, SH& sh, const f
         }
     }
     return true;
-}
-
-// ---------------------------------------------------------------------------
-// The k16 sweep, software-pipelined (MfmaSpec::pipe; full waves: both 32-ray
-// blocks).  A 32-ray block (G, R) is two steps: P1 = the six U V X products,
-// P2 = the -tn and Y products.  Its reduction is two steps as well: r1 = the
-// max of U V X (16 v_max3), r2 = the max with -tn and Y and the min over the
-// lane's pairs (24 VALU).  The stream pairs each product step with the
-// reduction step whose inputs are complete:
-//   P1(G,R) | r2 of the previous block      P2(G,R) | r1(G,R)
-// one MFMA, then up to four (P1) or eight (P2) VALU
-// (__builtin_amdgcn_sched_group_barrier), so that one wave's matrix pipe and
-// VALU port work side by side instead of in turn, with at most 96 accumulator
-// VGPRs live.  The next group's records are requested at the start of a group
-// into a second operand set.  Group G's tmin is complete after P1(G+1, 0)'s
-// step; its ballot and exact phase (sweep_k16's: index order, the reference
-// arithmetic) run there, before any Y product of group G+1, so every Y term
-// reads the bound of all groups before its own, as in sweep_k16.
-template <MfmaSpec S, class SH>
-__device__ __forceinline__ bool sweep_k16_pipe(const RenderParams& p, SH& sh, const f3& o, const f3& d, float& best,
-                                               int& bi, float& bestK, MfmaDiag& dg) {
-    static_assert(S.k16 && S.ymma && S.imax && S.minred, "the pipelined k16 sweep implements the k16 ymma / minred form");
-    static_assert(!S.k5 || (!S.prefetch && !S.lateload && !S.afrag_lds && (S.serial == 1 || S.serial == 3 || S.serial == 4)),
-                  "the 5-product form is built on the serialised sweep");
-    const int lane = (int)lane_id();
-    const int r32 = lane & 31, hl = lane >> 5;
-    const f3 m = cross(d, o);
-    MfmaScale sc;
-    if (!mfma_scale<S>(p.mfma_A, o, d, m, sc)) return false;
-    mfma_main_row(&sh.ray[lane][0], d, m, o, sc.sigma);
-    // k5: the wave's largest |ray lo| and |ray hi| of m.z (slots 16 and 17 of
-    // the main fragment, the same arithmetic as mfma_main_row): with the
-    // records' per-triangle |hi|, |lo| of the m.z coefficients they bound the
-    // two products the 5-product form leaves out of U, -V and X
-    [[maybe_unused]] float zlo = 0.0f, zhi = 0.0f;
-    if constexpr (S.k5) {
-        const float vz = m.z * sc.sigma;
-        const _Float16 hz = (_Float16)vz;
-        const _Float16 lz = (_Float16)(vz - (float)hz);
-        zhi = wave_max(fabsf((float)hz));
-        zlo = wave_max(fabsf((float)lz));
-    }
-    auto write_y = [&](float bkv) {
-        _Float16 s[16];
-        mfma_y_chunk(s, d, o, bkv, sc.sigma, sc.Bmax);
-        h8* row = reinterpret_cast<h8*>(&sh.ray[lane][32]);
-        row[0] = h8{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7]};
-        row[1] = h8{s[8], s[9], s[10], s[11], s[12], s[13], s[14], s[15]};
-    };
-    write_y(bestK);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    h8 a0[2], a1[2], y1[2];
-#pragma unroll
-    for (int R = 0; R < 2; R++) {
-        a0[R] = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][8 * hl]);
-        a1[R] = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][16 + 8 * hl]);
-    }
-    auto read_y = [&]() {
-#pragma unroll
-        for (int R = 0; R < 2; R++) y1[R] = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][32 + 8 * hl]);
-    };
-    read_y();
-
-    const int ng = (p.n_tris + 31) >> 5;
-    if (ng == 0) return true;
-    const h8* fg0 = reinterpret_cast<const h8*>(p.mfma_k16_frag) + lane;
-    const float* tg0 = p.mfma_k16_tau + r32;
-    // group g's records (g clamped to the last group: the loads past the end are
-    // harmless re-reads, so that the pipelined region has no branch)
-    auto fetch = [&](int g, h8* dst, float& t) {
-        g = min(g, ng - 1);
-        const h8* f = fg0 + (size_t)g * (kK16Ops * 64);
-#pragma unroll
-        for (int op = 0; op < kK16Ops; op++) dst[op] = f[64 * op];
-        t = tg0[32 * g];
-    };
-    auto p1 = [&](int R, const h8* b, f16v& U, f16v& V, f16v& X) {
-        const f16v zero = {};
-        U = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[R], b[0], zero, 0, 0, 0);
-        V = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[R], b[2], zero, 0, 0, 0);
-        X = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[R], b[4], zero, 0, 0, 0);
-        U = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[R], b[1], U, 0, 0, 0);
-        V = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[R], b[3], V, 0, 0, 0);
-        X = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[R], b[5], X, 0, 0, 0);
-    };
-    auto p2 = [&](int R, const h8* b, f16v& T, f16v& Y) {
-        const f16v zero = {};
-        T = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[R], b[6], zero, 0, 0, 0);
-        Y = __builtin_amdgcn_mfma_f32_32x32x16_f16(y1[R], b[6], zero, 0, 0, 0);
-    };
-    auto r1 = [&](const f16v& U, const f16v& V, const f16v& X, int* t3) {
-#pragma unroll
-        for (int i = 0; i < 16; i++)
-            t3[i] = max(max(__float_as_int(U[i]), __float_as_int(V[i])), __float_as_int(X[i]));
-    };
-    auto r2 = [&](const int* t3, const f16v& T, const f16v& Y, int tm) {
-#pragma unroll
-        for (int i = 0; i < 16; i++) tm = min(tm, max(max(t3[i], __float_as_int(T[i])), __float_as_int(Y[i])));
-        return tm;
-    };
-    auto il_p1 = [&]() {
-#pragma unroll
-        for (int k = 0; k < 6; k++) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-        }
-    };
-    auto il_p2 = [&]() {
-#pragma unroll
-        for (int k = 0; k < 2; k++) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
-        }
-    };
-    // exact phase of group g (its ballot mask M), sweep_k16's
-    auto exact = [&](int g, unsigned long long M) {
-        if constexpr (S.diag) dg.groups += 1;
-        if (!M) return;
-        if constexpr (S.diag) dg.hot += 1;
-        uint32_t m32 = (uint32_t)(M | M >> 32);
-        const float bk0 = bestK;
-        while (m32) {
-            const int t = __builtin_ctz(m32);
-            m32 &= m32 - 1;
-            const int idx = 32 * g + t;
-            if (idx >= p.n_tris) break;
-            if constexpr (S.diag) dg.exact += 1;
-            cfloat* tp = (cfloat*)p.tri + 12 * idx;
-            const MtQ qq = mt_quantities(o, d, ldc4(tp), ldc4(tp + 4), ldc4(tp + 8));
-            if (mt_pass3(qq, bestK)) mt_exact(qq, idx, best, bi, bestK);
-        }
-        if (__ballot(bestK != bk0)) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            write_y(bestK);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            read_y();
-        }
-    };
-
-    h8 bA[kK16Ops], bB[kK16Ops];
-    float tauA, tauB;
-    // carried between steps: the previous block's U V X max and -tn, Y terms
-    int t3[16];
-    f16v T = {}, Y = {};
-#pragma unroll
-    for (int i = 0; i < 16; i++) t3[i] = 0x7f7fffff;  // "block (-1, 1)": passes nothing
-    int tmin0 = 0x7fffffff;  // the current group's minimum over its block 0
-    float Tl_prev = 0.0f;
-    fetch(0, bA, tauA);
-    // group g with records cur (tau tc); nxt receives group g+1's
-    auto group = [&](int g, const h8* cur, float tc, h8* nxt, float& tn) {
-        f16v U, V, X;
-        // P1(g, 0) | r2(g-1, 1); group g+1's records requested
-        __builtin_amdgcn_sched_barrier(0);
-        fetch(g + 1, nxt, tn);
-        p1(0, cur, U, V, X);
-        const int tprev = r2(t3, T, Y, tmin0);
-        il_p1();
-        __builtin_amdgcn_sched_barrier(0);
-        if (g > 0) exact(g - 1, __ballot(tprev <= __float_as_int(Tl_prev)));
-        // P2(g, 0) | r1(g, 0)
-        __builtin_amdgcn_sched_barrier(0);
-        p2(0, cur, T, Y);
-        r1(U, V, X, t3);
-        il_p2();
-        __builtin_amdgcn_sched_barrier(0);
-        // P1(g, 1) | r2(g, 0)
-        p1(1, cur, U, V, X);
-        tmin0 = r2(t3, T, Y, 0x7fffffff);
-        il_p1();
-        __builtin_amdgcn_sched_barrier(0);
-        // P2(g, 1) | r1(g, 1)
-        p2(1, cur, T, Y);
-        r1(U, V, X, t3);
-        il_p2();
-        __builtin_amdgcn_sched_barrier(0);
-        Tl_prev = tc * sc.Tw;
-    };
-    int G = 0;
-    for (; G + 1 < ng; G += 2) {
-        group(G, bA, tauA, bB, tauB);
-        group(G + 1, bB, tauB, bA, tauA);
-    }
-    if (G < ng) group(G, bA, tauA, bB, tauB);
-    // drain: r2 of the last group's block 1
-    const int tlast = r2(t3, T, Y, tmin0);
-    exact(ng - 1, __ballot(tlast <= __float_as_int(Tl_prev)));
-    return true;
-}
-
-// ---------------------------------------------------------------------------
-// The k16 sweep with workgroup-shared LDS record tiles (render_mfma_tiled;
-// scenes whose records outgrow the L2: config C's 100k and config E's 1M
-// triangles, 7 KiB of records per 32 triangles).  The workgroup's waves sweep
-// the same records in the same order, so each tile of tile_groups groups is
-// brought into LDS once per workgroup — by LDS-DMA (global_load_lds_dwordx4:
-// no VGPRs, coalesced 1-KiB pieces split across the waves), double-buffered so
-// that tile t+1 is in flight while tile t is swept — instead of once per wave
-// from L2/MALL: 1/NW of the record traffic.  One barrier per tile.  Every wave
-// of the workgroup runs the tile loop (its barriers) in every segment; only
-// waves with rays of their own in the filter's range compute (`sweeping`).
-// The arithmetic is sweep_k16's, term for term.
-template <MfmaSpec S>
-__device__ __forceinline__ bool sweep_k16_tiles(const RenderParams& p, MfmaK16Lds& sh, h8 (*tiles)[S.tile_groups * kK16Ops * 64],
-                                                float (*ttau)[(S.tile_groups * 32 + 63) / 64 * 64], const f3& o,
-                                                const f3& d, float& best, int& bi, float& bestK, MfmaDiag& dg,
-                                                bool sweeping) {
-    static_assert(S.ymma && S.imax && S.minred && S.k16 && S.tile_groups > 0, "k16 ymma/imax/minred form");
-    constexpr int K = S.tile_groups, NW = S.block / 64;
-    const int lane = (int)lane_id();
-    const int r32 = lane & 31, hl = lane >> 5, wave = (int)(threadIdx.x >> 6);
-    MfmaScale sc{0.0f, 0.0f, 0.0f};
-    h8 a0[2], a1[2], y1[2];
-    bool compute = false, in_range = true;
-    auto write_y = [&](float bkv) {
-        _Float16 s[16];
-        mfma_y_chunk(s, d, o, bkv, sc.sigma, sc.Bmax);
-        h8* row = reinterpret_cast<h8*>(&sh.ray[lane][32]);
-        row[0] = h8{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7]};
-        row[1] = h8{s[8], s[9], s[10], s[11], s[12], s[13], s[14], s[15]};
-    };
-    auto read_y = [&]() {
-#pragma unroll
-        for (int R = 0; R < 2; R++) y1[R] = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][32 + 8 * hl]);
-    };
-    if (sweeping) {
-        const f3 m = cross(d, o);
-        in_range = mfma_scale<S>(p.mfma_A, o, d, m, sc);
-        if (in_range) {
-            mfma_main_row(&sh.ray[lane][0], d, m, o, sc.sigma);
-            write_y(bestK);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-            for (int R = 0; R < 2; R++) {
-                a0[R] = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][8 * hl]);
-                a1[R] = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][16 + 8 * hl]);
-            }
-            read_y();
-            compute = true;
-        }
-    }
-    const int ng = (p.n_tris + 31) >> 5, nt = (ng + K - 1) / K;
-    const int n_tau = ng * 32;
-    const h8* gsrc = reinterpret_cast<const h8*>(p.mfma_k16_frag);
-    // LDS-DMA of tile t into buffer t&1: 1-KiB record pieces (a lane's 16 B
-    // land at base + 16 lane) and 256-B tau pieces, round-robin over the waves
-    auto issue = [&](int t) {
-        const int g0 = t * K, gn = min(K, ng - g0), pieces = gn * kK16Ops, tp = (gn * 32 + 63) / 64;
-        for (int pc = wave; pc < pieces + tp; pc += NW) {
-            if (pc < pieces) {
-                __builtin_amdgcn_global_load_lds(
-                    (const __attribute__((address_space(1))) void*)(gsrc + ((size_t)g0 * kK16Ops + pc) * 64 + lane),
-                    (__attribute__((address_space(3))) void*)&tiles[t & 1][pc * 64], 16, 0, 0);
-            } else {
-                const int q = pc - pieces, idx = min(32 * g0 + 64 * q + lane, n_tau - 1);
-                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(p.mfma_k16_tau + idx),
-                                                 (__attribute__((address_space(3))) void*)&ttau[t & 1][64 * q], 4, 0,
-                                                 0);
-            }
-        }
-    };
-    issue(0);
-    for (int t = 0; t < nt; t++) {
-        __syncthreads();  // tile t has landed (every wave's DMA), every wave is done with tile t-1's buffer
-        if (t + 1 < nt) issue(t + 1);
-        if (!compute) continue;
-        const int gn = min(K, ng - t * K);
-        for (int gi = 0; gi < gn; gi++) {
-            const int G = t * K + gi;
-            h8 b[kK16Ops];
-#pragma unroll
-            for (int op = 0; op < kK16Ops; op++) b[op] = tiles[t & 1][(gi * kK16Ops + op) * 64 + lane];
-            const float Tl = ttau[t & 1][gi * 32 + r32] * sc.Tw;
-            int tmin = 0x7fffffff;
-#pragma unroll
-            for (int R = 0; R < 2; R++) {
-                const K16Terms q = k16_terms(a0[R], a1[R], y1[R], b);
-#pragma unroll
-                for (int i = 0; i < 16; i++) {
-                    const int t3 = max(max(__float_as_int(q.U[i]), __float_as_int(q.V[i])), __float_as_int(q.X[i]));
-                    tmin = min(tmin, max(max(t3, __float_as_int(q.T[i])), __float_as_int(q.Y[i])));
-                }
-            }
-            const unsigned long long M = __ballot(tmin <= __float_as_int(Tl));
-            if constexpr (S.diag) dg.groups += 1;
-            if (M) {
-                if constexpr (S.diag) dg.hot += 1;
-                uint32_t m32 = (uint32_t)(M | M >> 32);
-                const float bk0 = bestK;
-                while (m32) {
-                    const int tt = __builtin_ctz(m32);
-                    m32 &= m32 - 1;
-                    const int idx = 32 * G + tt;
-                    if (idx >= p.n_tris) break;
-                    if constexpr (S.diag) dg.exact += 1;
-                    cfloat* tp = (cfloat*)p.tri + 12 * idx;
-                    const MtQ qq = mt_quantities(o, d, ldc4(tp), ldc4(tp + 4), ldc4(tp + 8));
-                    if (mt_pass3(qq, bestK)) mt_exact(qq, idx, best, bi, bestK);
-                }
-                if (__ballot(bestK != bk0)) {
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    write_y(bestK);
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    read_y();
-                }
-            }
-        }
-    }
-    return in_range;
 }
 
 // ---------------------------------------------------------------------------
@@ -1489,97 +1162,6 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
             atomicAdd(p.seg_counter + 1, dg.groups);  // (wave, triangle group) sweeps
             atomicAdd(p.seg_counter + 2, dg.hot);     // ... with a passing pair
             atomicAdd(p.seg_counter + 3, dg.exact);   // (wave, triangle) exact tests
-            atomicAdd(p.seg_counter + 8, dg.t_advance);
-            atomicAdd(p.seg_counter + 9, dg.t_sweep);
-            atomicAdd(p.seg_counter + 10, dg.t_shade);
-            atomicAdd(p.seg_counter + 11, dg.t_tail);
-        }
-}
-
-// render_mfma with workgroup-shared LDS record tiles (sweep_k16_tiles): the
-// same lockstep segment loop, but every wave of the workgroup enters the tile
-// loop in every segment (its barriers), then the cooperative drain, the
-// scalar-path fallback and the shading as in render_mfma.
-template <MfmaSpec S>
-__global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves))) void render_mfma_tiled(RenderParams p) {
-    constexpr int K = S.tile_groups;
-    __shared__ MfmaK16Lds wl[S.block / 64];
-    __shared__ h8 tiles[2][K * kK16Ops * 64];
-    __shared__ float ttau[2][(K * 32 + 63) / 64 * 64];
-    MfmaK16Lds& sh = wl[threadIdx.x >> 6];
-    Lane L;
-    lane_init(L);
-    MfmaDiag dg;
-    unsigned long long tc = 0;
-    if constexpr (S.diag) tc = __builtin_amdgcn_s_memtime();
-    auto stamp = [&](unsigned long long& acc) {
-        if constexpr (S.diag) {
-            const unsigned long long t = __builtin_amdgcn_s_memtime();
-            acc += t - tc;
-            tc = t;
-        }
-    };
-    for (;;) {
-        advance(L, p);
-        const unsigned long long act = __ballot(L.st == ST_TRACE);
-        stamp(dg.t_advance);
-        if (!__syncthreads_or(act != 0)) break;  // workgroup-uniform: every wave leaves together
-        const bool coop = act != 0 && __popcll(act) <= (unsigned)S.tail_lanes && __any(L.st == ST_DONE);
-        const bool sweeping = act != 0 && !coop;
-        const bool mine = L.st == ST_TRACE;
-        f3 ro = L.o, rd = L.d;
-        if (sweeping) {  // lanes without a ray carry the first live lane's (their passes add no triangle)
-            const int j0 = __builtin_ctzll(act);
-            const f3 o = mk(__shfl(L.o.x, j0), __shfl(L.o.y, j0), __shfl(L.o.z, j0));
-            const f3 dd = mk(__shfl(L.d.x, j0), __shfl(L.d.y, j0), __shfl(L.d.z, j0));
-            ro = mine ? L.o : o;
-            rd = mine ? L.d : dd;
-        }
-        float best = 1e38f, bestK = 1e38f * 1.0009765625f;
-        int bi = -1;
-        const bool swept = sweep_k16_tiles<S>(p, sh, tiles, ttau, ro, rd, best, bi, bestK, dg, sweeping);
-        stamp(dg.t_sweep);
-        if (coop) {
-            float mybest = 1e38f;
-            int mybi = -1;
-            unsigned long long mm = act;
-            while (mm) {
-                const int j = __builtin_ctzll(mm);
-                mm &= mm - 1;
-                const f3 oj = mk(__shfl(L.o.x, j), __shfl(L.o.y, j), __shfl(L.o.z, j));
-                const f3 dj = mk(__shfl(L.d.x, j), __shfl(L.d.y, j), __shfl(L.d.z, j));
-                float b;
-                int bidx;
-                coop_closest(oj, dj, p.tri, p.n_tris, b, bidx);
-                if ((int)lane_id() == j) {
-                    mybest = b;
-                    mybi = bidx;
-                }
-            }
-            if (mine) {
-                L.bounce += 1;
-                L.segs += 1;
-                shade(L, p, mybest, mybi);
-            }
-            stamp(dg.t_tail);
-            continue;
-        }
-        if (!act) continue;
-        if (!swept && mine)
-            sweep_masked<8, true, Filter::Max3>(ro, rd, nullptr, (const float*)p.tri, p.n_tris, 0, best, bi, bestK);
-        if (mine) {
-            L.bounce += 1;
-            L.segs += 1;
-            shade(L, p, best, bi);
-        }
-        stamp(dg.t_shade);
-    }
-    flush_counters(L, p);
-    if constexpr (S.diag)
-        if (lane_id() == 0) {
-            atomicAdd(p.seg_counter + 1, dg.groups);
-            atomicAdd(p.seg_counter + 2, dg.hot);
-            atomicAdd(p.seg_counter + 3, dg.exact);
             atomicAdd(p.seg_counter + 8, dg.t_advance);
             atomicAdd(p.seg_counter + 9, dg.t_sweep);
             atomicAdd(p.seg_counter + 10, dg.t_shade);

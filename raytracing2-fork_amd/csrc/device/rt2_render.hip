@@ -39,9 +39,6 @@ using namespace rt2d;
 #include "rt2_brute.h"
 #include "rt2_mfma.h"
 #include "rt2_k5_tiles.h"
-#ifdef RT2_EXPERIMENTS
-#include "rt2_mfma32.h"
-#endif
 #include "rt2_assist.h"
 #include "rt2_bvh.h"
 #include "rt2_misc_kernels.h"
@@ -413,30 +410,46 @@ static int scene_init(rt2_scene* s, const rt2_triangle* tris, int32_t n_tris, co
         s->plk_ok = (unsigned long long)flags[0] * 64 <= (unsigned long long)n_tris;  // <= 1/64 always-pass records
         std::memcpy(&s->plk_A, &flags[1], sizeof(float));
 #endif
-        // matrix-core filter records (render_mfma): 5 KiB per 16 triangles
-        const int n_pad = (n_tris + 15) / 16 * 16;
-        HIPCHECK(hipMalloc(&s->d_mfma, (size_t)n_pad * kMfmaQ * 32 * sizeof(_Float16)));
-        HIPCHECK(hipMalloc(&s->d_mfma_tau, (size_t)n_pad * sizeof(float)));
+        // matrix-core filter records in the k16 layout (sweep_k16 and its
+        // 5-product form): 7 KiB per 32 triangles; the prep's flags give the
+        // scene's largest |a_i|, the filter's range check.  (The 16x16x32
+        // layout of the experiment variants and the probe's layout 0 is built
+        // on first use: ensure_mfma16.)
+        const int n_pad32 = (n_tris + 31) / 32 * 32;
+        HIPCHECK(hipMalloc(&s->d_mfma_k16, (size_t)n_pad32 * kK16Ops * 16 * sizeof(_Float16)));
+        HIPCHECK(hipMalloc(&s->d_mfma_k16_tau, (size_t)n_pad32 * sizeof(float)));
+        HIPCHECK(hipMalloc(&s->d_mfma_k16_bnd, (size_t)n_pad32 * sizeof(float2)));
         uint32_t* d_mflags = reinterpret_cast<uint32_t*>(s->d_counters + kCounters - 2);
         HIPCHECK(hipMemset(d_mflags, 0, 2 * sizeof(uint32_t)));
-        hipLaunchKernelGGL(prep_mfma, dim3((n_pad + 255) / 256), dim3(256), 0, 0, s->d_tri, n_tris, n_pad, s->d_mfma,
-                           s->d_mfma_tau, d_mflags);
+        hipLaunchKernelGGL(prep_mfma_k16, dim3((n_pad32 + 255) / 256), dim3(256), 0, 0, s->d_tri, n_tris, n_pad32,
+                           s->d_mfma_k16, s->d_mfma_k16_tau, s->d_mfma_k16_bnd, d_mflags);
         HIPCHECK(hipGetLastError());
         uint32_t mflags[2];
         HIPCHECK(hipMemcpy(mflags, d_mflags, sizeof(mflags), hipMemcpyDeviceToHost));
         HIPCHECK(hipMemset(d_mflags, 0, 2 * sizeof(uint32_t)));
         std::memcpy(&s->mfma_A, &mflags[1], sizeof(float));
         s->mfma_ok = s->mfma_A <= 0x1p20f;
-        // the same coefficients in the k16 layout (sweep_k16): 7 KiB per 32 triangles
-        const int n_pad32 = (n_tris + 31) / 32 * 32;
-        HIPCHECK(hipMalloc(&s->d_mfma_k16, (size_t)n_pad32 * kK16Ops * 16 * sizeof(_Float16)));
-        HIPCHECK(hipMalloc(&s->d_mfma_k16_tau, (size_t)n_pad32 * sizeof(float)));
-        HIPCHECK(hipMalloc(&s->d_mfma_k16_bnd, (size_t)n_pad32 * sizeof(float2)));
-        hipLaunchKernelGGL(prep_mfma_k16, dim3((n_pad32 + 255) / 256), dim3(256), 0, 0, s->d_tri, n_tris, n_pad32,
-                           s->d_mfma_k16, s->d_mfma_k16_tau, s->d_mfma_k16_bnd, d_mflags);
-        HIPCHECK(hipGetLastError());
-        HIPCHECK(hipMemset(d_mflags, 0, 2 * sizeof(uint32_t)));
     }
+    HIPCHECK(hipDeviceSynchronize());
+    return 0;
+}
+
+// The 16x16x32 record layout (5 KiB per 16 triangles: the experiment
+// variants of that form and the filter probe's layout 0), built on first use
+// so that a product scene does not keep 320 B per triangle it never reads.
+static int ensure_mfma16(rt2_scene* s) {
+    if (s->d_mfma || s->n_tris <= 0) return 0;
+    HIPCHECK(hipSetDevice(s->device));
+    const int n_pad = (s->n_tris + 15) / 16 * 16;
+    HIPCHECK(hipMalloc(&s->d_mfma, (size_t)n_pad * kMfmaQ * 32 * sizeof(_Float16)));
+    HIPCHECK(hipMalloc(&s->d_mfma_tau, (size_t)n_pad * sizeof(float)));
+    HIPCHECK(hipDeviceSynchronize());  // the scratch flags below are the counters' last two words
+    uint32_t* d_mflags = reinterpret_cast<uint32_t*>(s->d_counters + kCounters - 2);
+    HIPCHECK(hipMemset(d_mflags, 0, 2 * sizeof(uint32_t)));
+    hipLaunchKernelGGL(prep_mfma, dim3((n_pad + 255) / 256), dim3(256), 0, 0, s->d_tri, s->n_tris, n_pad, s->d_mfma,
+                       s->d_mfma_tau, d_mflags);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipMemset(d_mflags, 0, 2 * sizeof(uint32_t)));
     HIPCHECK(hipDeviceSynchronize());
     return 0;
 }
@@ -535,8 +548,6 @@ constexpr AssistSpec assist12_x(int coop) {
 #endif
 constexpr TiledSpec kTiledLarge{.block = 512, .group = 4, .filter = Filter::Max3};
 constexpr AssistSpec kAssist12{.waves_per_block = 12, .group = 8, .filter = Filter::Max3, .waves = 6, .coop_rays = 32};
-constexpr MfmaSpec kMfmaT8Y{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true, .ymma = true,
-                            .tshift = 12};
 constexpr MfmaSpec kMfmaT8Y4{.block = 256, .waves = 4, .tail_lanes = 8, .imax = true, .minred = true, .ymma = true,
                              .tshift = 12};
 // k16 sweep (v_mfma_f32_32x32x16_f16, 8 products per 1,024 pairs)
@@ -602,6 +613,8 @@ constexpr MfmaSpec k5_tiles_spec(int K, bool no_tn, int tail, bool diag = false)
 constexpr Bvh3Spec kBvhDefault{.block = 256, .thresh = 16, .slab = Slab::Markstein, .waves = 5, .diag = false};
 
 #ifdef RT2_EXPERIMENTS
+constexpr MfmaSpec kMfmaT8Y{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true, .ymma = true,
+                            .tshift = 12};
 constexpr MfmaSpec kMfmaT8Y4D{.block = 256, .waves = 4, .tail_lanes = 8, .imax = true, .minred = true, .diag = true,
                               .ymma = true, .tshift = 12};
 constexpr MfmaSpec kMfmaT8{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true};
@@ -651,13 +664,7 @@ const Variant kVariants[] = {
     RT2_VARIANT(109, K_BVH4, render_bvh4<kBvhDefault>, 256, "bvh4/256/t16/w5"),           // default (BVH traversal)
     RT2_VARIANT(86, K_TILED, render_tiled<kTiledLarge>, 512, "tiled/512/max3f4"),          // > kSmemMaxTris
     RT2_VARIANT(92, K_ASSIST, render_assist<kAssist12>, 768, "assist12/max3f8/w6"),        // < 4 items per lane
-    RT2_VARIANT(152, K_MFMA, render_mfma<kMfmaT8Y4>, 256, "mfma/256/f16x3/coop8/w4/imax/minred/ymma/t12"),  // default (<= kMfmaMaxTris)
-    RT2_VARIANT(150, K_MFMA, render_mfma<kMfmaT8Y>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma/t12"),  // 1.5-3 items per lane
     RT2_VARIANT(136, K_SMEM, render_smem<kSmemDefault>, 256, "smem/256/max3f8/coop32/w6/lockstep"),  // variant 0 forced (id 0 = automatic)
-    // default brute-force kernel for every scene in the matrix filter's range (DESIGN.md "The k16 sweep")
-    RT2_VARIANT(200, K_MFMA, render_mfma<kMfmaK16>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"),
-    // the same at 4 waves per SIMD (path state packed into 15 LDS words): rank slabs with < 1.5 items per 3-wave lane
-    RT2_VARIANT(206, K_MFMA, render_mfma<kMfmaK16W4>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
     // default brute-force kernel (DESIGN.md "The 5-product form"): the k16 sweep with U, -V, X from the first K-half,
     // the left-out m.z slots bounded in the threshold; 3 waves per SIMD, and 4 for launches with < 1.5 items per lane
     RT2_VARIANT(227, K_MFMA, render_mfma<kMfmaK5>, 256, "mfma/256/k5/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"),
@@ -672,6 +679,11 @@ const Variant kVariants[] = {
     RT2_VARIANT(250, K_MFMA, render_mfma_k5t<k5_tiles_spec(4, false, 0)>, 768, "mfmat5/768/k5/tile4/coop0/w3/llds2/cmp"),
     RT2_VARIANT(252, K_MFMA, render_mfma_k5t<k5_tiles_spec(4, true, 0)>, 768, "mfmat5/768/k5/notn/tile4/coop0/w3/llds2/cmp"),
 #ifdef RT2_EXPERIMENTS
+    // earlier product kernels (round 2's 16x16x32 form; round 3's k16 sweep), kept for A/B
+    RT2_VARIANT(152, K_MFMA, render_mfma<kMfmaT8Y4>, 256, "mfma/256/f16x3/coop8/w4/imax/minred/ymma/t12"),
+    RT2_VARIANT(150, K_MFMA, render_mfma<kMfmaT8Y>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma/t12"),
+    RT2_VARIANT(200, K_MFMA, render_mfma<kMfmaK16>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"),
+    RT2_VARIANT(206, K_MFMA, render_mfma<kMfmaK16W4>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
     RT2_VARIANT(251, K_MFMA, render_mfma_k5t<k5_tiles_spec(4, false, 0, true)>, 768, "mfmat5/768/k5/tile4/coop0/w3/llds2/cmp/diag"),
     RT2_VARIANT(253, K_MFMA, render_mfma_k5t<k5_tiles_spec(2, false, 0)>, 768, "mfmat5/768/k5/tile2/coop0/w3/llds2/cmp"),
     RT2_VARIANT(254, K_MFMA, render_mfma_k5t<k5_tiles_spec(4, false, 8)>, 768, "mfmat5/768/k5/tile4/coop8/w3/llds2/cmp"),
@@ -700,10 +712,6 @@ const Variant kVariants[] = {
     RT2_VARIANT(182, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3); x.serial = 2; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/ser2"),
     RT2_VARIANT(183, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(4); x.serial = 1; return x; }()>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/ser1"),
     RT2_VARIANT(184, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3, false, false, false, true); x.lane_lds = true; x.serial = 1; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/pf/llds/ser1"),
-    RT2_VARIANT(185, K_MFMA, render_mfma_tiled<[] { MfmaSpec x = k16_spec(3); x.tile_groups = 1; return x; }()>, 256, "mfmat/256/k16/tile1/w3"),
-    RT2_VARIANT(186, K_MFMA, render_mfma_tiled<[] { MfmaSpec x = k16_spec(3); x.block = 768; x.tile_groups = 4; return x; }()>, 768, "mfmat/768/k16/tile4/w3"),
-    RT2_VARIANT(187, K_MFMA, render_mfma_tiled<[] { MfmaSpec x = k16_spec(3, false, true); x.block = 768; x.tile_groups = 4; return x; }()>, 768, "mfmat/768/k16/tile4/w3/diag"),
-    RT2_VARIANT(188, K_MFMA, render_mfma_tiled<[] { MfmaSpec x = k16_spec(3); x.block = 512; x.tile_groups = 2; return x; }()>, 512, "mfmat/512/k16/tile2/w3"),
     RT2_VARIANT(189, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3); x.lane_lds = true; x.serial = 1; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser1"),
     RT2_VARIANT(193, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3, true, false, false, true); x.lane_lds = true; x.serial = 1; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/alds/pf/llds/ser1"),
     RT2_VARIANT(194, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3, true); x.serial = 1; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/alds/ser1"),
@@ -721,9 +729,6 @@ const Variant kVariants[] = {
     RT2_VARIANT(209, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.tshift = 8; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t8/llds/ser4/cmp"),
     RT2_VARIANT(210, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.diag = true; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp/diag"),
     RT2_VARIANT(211, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.diag = true; x.tshift = 8; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t8/llds/ser4/cmp/diag"),
-    RT2_VARIANT(212, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.pipe = true; x.waves = 2; return x; }()>, 256, "mfma/256/k16/coop8/w2/imax/minred/ymma/t12/llds/ser4/cmp/pipe"),
-    RT2_VARIANT(213, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.pipe = true; x.waves = 2; x.lane_lds = 0; return x; }()>, 256, "mfma/256/k16/coop8/w2/imax/minred/ymma/t12/ser4/cmp/pipe"),
-    RT2_VARIANT(214, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.pipe = true; x.diag = true; x.waves = 2; return x; }()>, 256, "mfma/256/k16/coop8/w2/imax/minred/ymma/t12/llds/ser4/cmp/pipe/diag"),
     RT2_VARIANT(222, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16W4; x.diag = true; return x; }()>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp/diag"),
     // the 5-product form (MfmaSpec::k5): U, -V, X from the first K-half, the m.z residual bounded in the threshold
     RT2_VARIANT(234, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4; x.serial = 1; return x; }()>, 256, "mfma/256/k5/notn/coop8/w4/imax/minred/ymma/t12/llds2/ser1/cmp"),
@@ -760,7 +765,6 @@ const Variant kVariants[] = {
     RT2_VARIANT(154, K_MFMA, render_mfma<kMfmaT8Y4T10>, 256, "mfma/256/f16x3/coop8/w4/imax/minred/ymma/t10"),  // T = 2^-10 R0
     RT2_VARIANT(155, K_MFMA, render_mfma<kMfmaT8Y4T14>, 256, "mfma/256/f16x3/coop8/w4/imax/minred/ymma/t14"),  // below the proven margin
     RT2_VARIANT(156, K_MFMA, render_mfma<kMfmaT8YDT12>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma/t12/diag"),
-    RT2_VARIANT(159, K_MFMA, render_mfma32<kMfmaT8Y>, 256, "mfma32/256/f16x3/coop8/w2/imax/minred/ymma/t12"),  // 32x32x16
     RT2_VARIANT(157, K_MFMA, render_mfma<kMfmaT8Y2W>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma/t12/occ2"),
     RT2_VARIANT(158, K_MFMA, render_mfma<kMfmaT8Y1W>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma/t12/occ1"),
     RT2_VARIANT(148, K_MFMA, render_mfma<kMfmaT8P3>, 256, "mfma/256/f16x3/coop8/w3/imax/minred/pf"),  // 140 + prefetch, 3 waves
@@ -1114,6 +1118,11 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
         VP = find_variant(vi);
     }
     const Variant& V = *VP;
+    if (std::strstr(V.name, "f16x3")) {  // the 16x16x32 record layout (experiment variants; built on first use)
+        if (ensure_mfma16(s) != 0) return -1;
+        p.mfma_frag = s->d_mfma;
+        p.mfma_tau = s->d_mfma_tau;
+    }
     // XCD-group item regions serve the BVH walk's L2 locality; the brute-force
     // kernels read the same records for every ray, so they take items from one
     // counter in dispatch order, which spreads neighbouring 64-pixel runs over
@@ -1374,6 +1383,7 @@ extern "C" long long rt2_scene_export(rt2_scene* s, int what, void* host, unsign
                  n32 = (size_t)(s->n_tris + 31) / 32 * 32;
     const void* src = nullptr;
     size_t sz = 0;
+    if ((what == 1 || what == 2) && ensure_mfma16(s) != 0) return -1;
     switch (what) {
     case 0: src = s->d_tri, sz = n * 3 * sizeof(float4); break;
     case 1: src = s->d_mfma, sz = n16 * kMfmaQ * 32 * sizeof(_Float16); break;
@@ -1409,6 +1419,7 @@ extern "C" int rt2_mfma_probe(rt2_scene* s, int layout, const float* rays, int32
         return -1;
     }
     HIPCHECK(hipSetDevice(s->device));
+    if (layout == 0 && ensure_mfma16(s) != 0) return -1;
     const int n_pad = layout >= 1 ? (s->n_tris + 31) / 32 * 32 : (s->n_tris + 15) / 16 * 16;
     const size_t nr = (size_t)n_rays;
     const size_t b_rays = nr * 8 * sizeof(float), b_terms = nr * n_pad * 5 * sizeof(float),

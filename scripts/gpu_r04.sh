@@ -9,6 +9,7 @@
 #   EVARIANTS=a,b      A/B on a config E sample (480x270, 4 spp)
 #   SVARIANTS=a,b      rank-slab probe of config B (scripts/shard_probe.py)
 #   BENCH=1            python bench.py (BENCH_ARGS)
+#   AB_LIB=exp         the A/B stages load the experiment build (rt2/librt2_exp.so)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
@@ -22,16 +23,16 @@ if [ -n "${PYTEST_K}" ]; then
   tail -2 gpurun_out/mfma_tests.log
 fi
 if [ -n "${VARIANTS}" ]; then
-  timeout -k 10 300 python scripts/ab_variants.py --config B --variants ${VARIANTS} --rounds ${ROUNDS:-3} > gpurun_out/ab_B.json 2>&1 || { echo "ab B failed"; tail -20 gpurun_out/ab_B.json; exit 1; }
+  RT2_LIB=${AB_LIB:-$RT2_LIB} timeout -k 10 300 python scripts/ab_variants.py --config B --variants ${VARIANTS} --rounds ${ROUNDS:-3} > gpurun_out/ab_B.json 2>&1 || { echo "ab B failed"; tail -20 gpurun_out/ab_B.json; exit 1; }
 fi
 if [ -n "${CVARIANTS}" ]; then
-  timeout -k 10 300 python scripts/ab_variants.py --config C --width 480 --height 270 --frames 2 --variants ${CVARIANTS} --rounds 2 > gpurun_out/ab_C.json 2>&1 || { echo "ab C failed"; tail -20 gpurun_out/ab_C.json; exit 1; }
+  RT2_LIB=${AB_LIB:-$RT2_LIB} timeout -k 10 300 python scripts/ab_variants.py --config C --width 480 --height 270 --frames 2 --variants ${CVARIANTS} --rounds 2 > gpurun_out/ab_C.json 2>&1 || { echo "ab C failed"; tail -20 gpurun_out/ab_C.json; exit 1; }
 fi
 if [ -n "${EVARIANTS}" ]; then
-  timeout -k 10 400 python scripts/ab_variants.py --config E --width 480 --height 270 --rays 4 --variants ${EVARIANTS} --rounds 2 > gpurun_out/ab_E.json 2>&1 || { echo "ab E failed"; tail -20 gpurun_out/ab_E.json; exit 1; }
+  RT2_LIB=${AB_LIB:-$RT2_LIB} timeout -k 10 400 python scripts/ab_variants.py --config E --width 480 --height 270 --rays 4 --variants ${EVARIANTS} --rounds 2 > gpurun_out/ab_E.json 2>&1 || { echo "ab E failed"; tail -20 gpurun_out/ab_E.json; exit 1; }
 fi
 if [ -n "${CFULL}" ]; then
-  timeout -k 10 500 python scripts/ab_variants.py --config C --variants ${CFULL} --rounds 1 > gpurun_out/ab_Cfull.json 2>&1 || { echo "ab C full failed"; tail -20 gpurun_out/ab_Cfull.json; exit 1; }
+  RT2_LIB=${AB_LIB:-$RT2_LIB} timeout -k 10 500 python scripts/ab_variants.py --config C --variants ${CFULL} --rounds 1 > gpurun_out/ab_Cfull.json 2>&1 || { echo "ab C full failed"; tail -20 gpurun_out/ab_Cfull.json; exit 1; }
 fi
 if [ -n "${SVARIANTS}" ]; then
   timeout -k 10 300 python scripts/shard_probe.py --variants ${SVARIANTS} > gpurun_out/shard_ab.log 2>&1 || { echo "shard probe failed"; tail -20 gpurun_out/shard_ab.log; exit 1; }

@@ -1,7 +1,8 @@
 """One rank of tests/test_gpu_multi.py::test_comm_two_ranks (run as a separate
 process per GPU): rt2_render_host_gather with uneven slabs and asymmetric
-8-bit output pointers, then rt2_gather_slabs, then a rank-local failure that
-every rank must see as an error instead of a hang.  Rank 0 writes its checks
+8-bit output pointers, then rt2_gather_slabs, then rank-local failures (a
+shard that does not match, and RT2_FAULT_AT injections at every site of
+rt2_comm_protocol.h) that every rank must see as an error instead of a hang.  Rank 0 writes its checks
 to the JSON file named on the command line."""
 import json
 import os
@@ -67,6 +68,36 @@ def main():
         res["failure_agreed"] = True
         res["failure_message"] = str(e)
     comm.check()
+    # injected failures (RT2_FAULT_AT, include/rt2.h "Failure contract"): a
+    # failure the agreement sees makes every rank return < 0 at once
+    for site in ("gather.prepare@1", "render@1", "check@0", "gather.prepare@0"):
+        os.environ["RT2_FAULT_AT"] = site
+        t0 = time.time()
+        try:
+            if site.startswith("gather."):
+                comm.gather_slabs(slab.data_ptr(), W, H, sh, 0, image.data_ptr() if rank == 0 else 0, stream)
+            else:
+                scene.render_host_gather(u, 0, 1, sh, comm, 0)
+            res[f"fault_{site}"] = False
+        except rt2.RT2Error:
+            res[f"fault_{site}"] = time.time() - t0 < 30
+        os.environ.pop("RT2_FAULT_AT")
+        comm.check()
+    # the communicator still works after them
+    got = scene.render_host_gather(u, 0, 1, sh, comm, 0)
+    if rank == 0:
+        res["after_faults"] = bool(np.array_equal(got, scene.render_host(u, 0, 1)))
+    # a rank that cannot take part in the agreement at all: it aborts, and the
+    # peers' watchdog aborts theirs at the deadline — every rank returns < 0
+    os.environ["RT2_FAULT_AT"] = "agree.copy@1"
+    os.environ["RT2_COMM_TIMEOUT_S"] = "10"
+    t0 = time.time()
+    try:
+        scene.render_host_gather(u, 0, 1, sh, comm, 0)
+        res["fault_agree.copy@1"] = False
+    except rt2.RT2Error:
+        res["fault_agree.copy@1"] = time.time() - t0 < 60
+    os.environ.pop("RT2_FAULT_AT")
     comm.close()
     if rank == 0:
         with open(out, "w") as f:

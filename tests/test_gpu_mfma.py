@@ -12,7 +12,7 @@ from test_gpu_parity import assert_exact, oracle_mean
 
 pytestmark = pytest.mark.gpu
 
-MFMA = 150
+MFMA = 227
 # product kernel: render_mfma (integer max of the terms, one compare per group,
 # cooperative drain at <= 8 live rays); experiment build: f32 max, a compare
 # per pair, record prefetch, 4 waves/SIMD, other drain thresholds,

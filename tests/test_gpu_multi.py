@@ -147,6 +147,42 @@ def test_comm_gather_slabs_one_rank(rt2mod, config_scene, torch_cuda):
     comm.close()
 
 
+@pytest.mark.parametrize("site", ["gather.prepare", "check", "render", "gather.issue", "agree.copy"])
+def test_comm_one_rank_injected_faults(rt2mod, config_scene, torch_cuda, site, monkeypatch):
+    """The failure sites of rt2_comm_protocol.h under RCCL (RT2_FAULT_AT): the
+    call returns < 0 within seconds; after the sites the agreement catches the
+    communicator still works, after gather.issue / agree.copy (the rank could
+    not take part) it was aborted and refuses further use."""
+    import time
+    torch = torch_cuda
+    sd, spec = config_scene("B")
+    W, H = 64, 30
+    u = rt2mod.offline_uniforms(W, H, spec.bounces, 2, sd.num_triangles)
+    scene = rt2mod.Scene(sd, 0)
+    slab = render_slab(rt2mod, torch, scene, u, 1, rt2mod.shard())
+    image = torch.zeros_like(slab)
+    stream = torch.cuda.current_stream().cuda_stream
+    comm = rt2mod.Comm(rt2mod.Comm.unique_id(), 1, 0, 0)
+    monkeypatch.setenv("RT2_FAULT_AT", site)
+    monkeypatch.setenv("RT2_COMM_TIMEOUT_S", "20")
+    t0 = time.time()
+    with pytest.raises(rt2mod.RT2Error):
+        if site == "gather.prepare":
+            comm.gather_slabs(slab.data_ptr(), W, H, rt2mod.shard(), 0, image.data_ptr(), stream)
+        else:
+            scene.render_host_gather(u, 0, 1, rt2mod.shard(), comm, 0)
+    assert time.time() - t0 < 20
+    monkeypatch.delenv("RT2_FAULT_AT")
+    if site in ("gather.issue", "agree.copy"):
+        with pytest.raises(rt2mod.RT2Error):
+            comm.check()
+    else:
+        comm.check()
+        img = scene.render_host_gather(u, 0, 1, rt2mod.shard(), comm, 0)
+        assert np.array_equal(img, scene.render_host(u, 0, 1))
+    comm.close()
+
+
 def test_torch_nccl_one_rank_gather(rt2mod, config_scene, torch_cuda):
     """bench.py's multi-GPU gather (rt2/dist.py gather_image: dist.gather on the
     nccl backend = RCCL) run for real on a one-rank process group: the gathered
@@ -203,4 +239,6 @@ def test_comm_two_ranks(rt2mod, tmp_path):
     import json
     res = json.load(open(out))
     assert res == {**res, "render_host_gather": True, "render_host_gather_rgb8": True, "gather_slabs": True,
-                   "failure_agreed": True}, res
+                   "failure_agreed": True, "fault_gather.prepare@1": True, "fault_render@1": True,
+                   "fault_check@0": True, "fault_gather.prepare@0": True, "after_faults": True,
+                   "fault_agree.copy@1": True}, res

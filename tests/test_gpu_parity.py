@@ -326,11 +326,11 @@ def test_frame_split_identical(rt2mod, oraclemod, config_scene, torch_cuda, trav
 
 
 # brute-force kernel variants that change the schedule, not the arithmetic:
-# the product variants (0 = automatic, 86, 92, 150/152/200/206 = the matrix filter, 136 = the scalar path
-# forced) and, in an experiment build, the A/B
+# the product variants (0 = automatic, 86, 92, 227/228/231/233/243 = the matrix filter, 250/252 = its LDS-tiled
+# form, 136 = the scalar path forced) and, in an experiment build, the A/B
 # variants (masked/plk filters, resident LDS, cooperative and team tail modes,
 # split waves, the round-1 slab kernels, occupancy hints)
-BRUTE_VARIANTS = [0, 86, 92, 150, 152, 200, 206, 227, 228, 231, 233, 136] + ([137, 138, 139, 140, 143, 144, 145, 146] if EXPERIMENTS else []) + ([22, 24, 28, 52, 64, 65, 66, 67, 68, 70, 71, 72, 73, 74, 76, 79, 80, 84, 85, 87, 89, 95, 97, 101, 104, 106,
+BRUTE_VARIANTS = [0, 86, 92, 227, 228, 231, 233, 243, 250, 252, 136] + ([150, 152, 200, 206, 137, 138, 139, 140, 143, 144, 145, 146] if EXPERIMENTS else []) + ([22, 24, 28, 52, 64, 65, 66, 67, 68, 70, 71, 72, 73, 74, 76, 79, 80, 84, 85, 87, 89, 95, 97, 101, 104, 106,
                                  90] if EXPERIMENTS else [])
 
 
