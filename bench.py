@@ -68,7 +68,7 @@ MFMA_K5_FLOP_PER_PAIR = 160   # its 5-product form (MfmaSpec::k5): 5 v_mfma_f32_
 MFMA_K5_NOTN_FLOP_PER_PAIR = 128  # ... without the -tn term (small scenes): 4 per 1,024 pairs
 SCALAR_VARIANT = 136       # render_smem forced (rt2_render.hip): the no-MFMA scalar-path kernel
 TARGET_RATIO = 10.0        # north star: >= 10x the CPU reference at config C on 1 GPU
-KERNEL_FILES = {"mfma": "render_mfma", "massist": "render_assist", "smem": "render_smem", "split": "render_split", "tiled": "render_tiled", "assist": "render_assist",
+KERNEL_FILES = {"mfmat5": "render_mfma_k5t", "mfma": "render_mfma", "massist": "render_assist", "smem": "render_smem", "split": "render_split", "tiled": "render_tiled", "assist": "render_assist",
                 "resident": "render_resident", "bvh4": "render_bvh4", "bvh3": "render_bvh3", "bvh2": "render_bvh2",
                 "bvh": "render_bvh"}
 
@@ -158,6 +158,7 @@ KERNEL_SOURCES = ["raytracing2-fork_amd/csrc/device/rt2_math.h", "raytracing2-fo
                   "raytracing2-fork_amd/csrc/device/rt2_path.h", "include/rt2_pinned_math.h", "include/rt2.h"]
 KERNEL_SOURCES_BY_TRAVERSAL = {"brute": ["raytracing2-fork_amd/csrc/device/rt2_brute.h",  # the brute-force kernels
                                          "raytracing2-fork_amd/csrc/device/rt2_mfma.h",
+                                         "raytracing2-fork_amd/csrc/device/rt2_k5_tiles.h",
                                          "raytracing2-fork_amd/csrc/device/rt2_assist.h"],
                                "bvh": ["raytracing2-fork_amd/csrc/device/rt2_bvh.h"]}
 

@@ -835,12 +835,15 @@ constexpr int kDefaultBvh = 109;
 constexpr int kLargeScene = 86;  // tiled/512/max3f4: LDS tiles above kSmemMaxTris triangles
 constexpr int kSlab = 92;        // assist12/max3f8/w6: fewer than 4 items per lane (multi-GPU slabs)
 constexpr int kMfmaSlabMaxTris = 8192;
-constexpr int kMfmaSmall = 233;    // <= kMfmaSlabMaxTris triangles: k5 without -tn, 4 waves (packed path state)
+constexpr int kMfmaSmall = 243;    // <= kMfmaSlabMaxTris triangles: k5 without -tn, 4 waves (packed path state),
+                                   // cooperative drain at <= 4 live rays (config B 187.9 vs 192.9 ms for 233's 8)
 constexpr int kMfmaSmallW3 = 231;  // ... 3 waves, when the packed fields cannot hold the launch
+constexpr int kMfmaTiles = 252;    // larger scenes: the 5-product form without -tn with workgroup-shared LDS record
+                                   // tiles (rt2_k5_tiles.h; DESIGN.md "LDS record tiles"): config C 26.94 vs 32.51 s
+                                   // for 227, config E sample 1.56 vs 2.53 s
 constexpr int kMfma = 227;  // mfma/.../k5/...: the matrix-core filter on v_mfma_f32_32x32x16_f16, 5 products per
-                            // 32-ray block (DESIGN.md "The 5-product form"): config B 214 vs 261 ms for the 8-product
-                            // k16 sweep (variant 200), config C sample 1.85 vs 2.08 s, config E sample 2.42 vs 2.63 s;
-                            // scenes above kMfmaSlabMaxTris triangles (smaller ones: kMfmaSmall)
+                            // 32-ray block (DESIGN.md "The 5-product form"), registers only; larger scenes whose
+                            // packed path state cannot hold the launch
 
 constexpr bool is_bvh(int kind) { return kind >= K_BVH && kind <= K_BVH4; }
 
@@ -1091,15 +1094,22 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
             vi = kMfma;
             // scenes whose records stay L2-resident (<= 8,192 triangles: config
             // B): without the -tn term, whose exact tests cost less there than
-            // its product (config B 195 vs 214 ms; on config E's closed mirror
-            // box it pays: +9 % without it), and at 4 waves per SIMD, which
+            // its product (config B 195 vs 214 ms), and at 4 waves per SIMD, which
             // packs the path state into 16-bit fields (x, y, rays per pixel)
             // and 12 bits of bounce count: whole images and rank slabs alike
             // (config B 195 vs 200 ms at 3 waves; 1/8 slab 29.4 vs 34.6 ms).
             // At config C's 100k triangles the fourth wave costs more than its
             // lanes gain (a 480x270x2 sample, 1.3 items per lane: 3.13 vs
             // 2.13 s for the k16 sweep)
-            if (s->n_tris <= kMfmaSlabMaxTris) vi = packed && find_variant(kMfmaSmall) ? kMfmaSmall : kMfmaSmallW3;
+            // Larger scenes stream their records from the MALL unless the
+            // workgroup shares them: the LDS-tiled kernel (one 12-wave
+            // workgroup per CU, packed path state), without the -tn term
+            // (config C 26.94 vs 29.19 s with it; config E sample 1.56 vs
+            // 1.60 s)
+            if (s->n_tris <= kMfmaSlabMaxTris)
+                vi = packed && find_variant(kMfmaSmall) ? kMfmaSmall : kMfmaSmallW3;
+            else if (packed && find_variant(kMfmaTiles))
+                vi = kMfmaTiles;
         } else if (vi == kDefaultBrute) {
             // scenes outside the matrix filter's range (mfma_ok = 0):
             // items per resident lane decide the tail: a lane ends on a whole
