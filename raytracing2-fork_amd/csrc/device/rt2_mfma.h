@@ -97,7 +97,12 @@ struct MfmaWaveLds {
 // coefficient in [2^13, 2^14)).  A triangle outside the validated range (as
 // sweep_plk's: |a_i| <= 2^20, e0/e1/n components 0 or in [2^-100, 2^20], max
 // >= 2^-30; non-finite) gets all-zero coefficients, which always pass (the
-// exact test decides); padding triangles get -tn = +2^13, which never passes.
+// exact test decides); padding triangles get -tn = +2^13, which never passes
+// in the forms that evaluate -tn.  The forms without it (MfmaSpec::no_tn:
+// variants 231/233/243/252) let padding pairs through (U = V = X = 0, Y <= 0);
+// their exact phase stops at idx >= n_tris before any triangle is read, so a
+// padding slot is never tested (tests/test_gpu_mfma.py test_range_edges: 1, 37
+// and 302 triangles, bit-exact on every variant).
 // flags[0] += out-of-range triangles, flags[1] = max |a_i| (float bits).
 // Shared by both record layouts (prep_mfma, prep_mfma_k16).
 struct MfmaCoef {

@@ -100,21 +100,28 @@ def _last_variant(rt2mod, scene):
     return rt2mod.lib().rt2_variant_name(lv.value).decode()
 
 
-AUTO_MFMA = "mfma/256/k5/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"  # variant 227 (the 5-product k16 form)
-AUTO_SMALL = "mfma/256/k5/notn/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp"  # 233: <= 8,192 triangles
+AUTO_TILES = "mfmat5/768/k5/notn/tile4/coop0/w3/llds2/cmp"  # variant 252: > 8,192 triangles, LDS record tiles
+AUTO_MFMA = "mfma/256/k5/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"  # 227: > 8,192 triangles, packed fields too small
+AUTO_SMALL = "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp"  # 243: <= 8,192 triangles
 AUTO_SMALL_W3 = "mfma/256/k5/notn/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"  # 231: packed fields too small
 
 
-def test_auto_variant_large_scene(rt2mod, config_scene, torch_cuda):
+def test_auto_variant_large_scene(rt2mod, oraclemod, config_scene, torch_cuda):
     """Scenes whose matrix-filter records outgrow an XCD's L2 (config C: 100k
-    triangles, 22 MB of k16 records) run the 5-product form with its -tn term
-    at 3 waves per SIMD, even below 1.5 items per lane (this small image): the
-    4-wave build without -tn serves only scenes of <= 8,192 triangles."""
+    triangles, 12.8 MB of k5 records) run the LDS-tiled 5-product form (one
+    12-wave workgroup per CU sharing each record tile), even on this small
+    image; a bounce limit the packed path state cannot hold takes the
+    register-only 3-wave build with -tn — same image either way."""
     sd, spec = config_scene("C")
     u = rt2mod.offline_uniforms(64, 36, spec.bounces, 1, sd.num_triangles)
     scene = rt2mod.Scene(sd, 0)
-    scene.render_host(u, 0, 1)
+    img = scene.render_host(u, 0, 1)
+    assert _last_variant(rt2mod, scene) == AUTO_TILES
+    u.maxBounceCount = 5000
+    img2 = scene.render_host(u, 0, 1)
     assert _last_variant(rt2mod, scene) == AUTO_MFMA
+    ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(0, 36, 5), 0, 1)
+    assert_exact(img2[::5], ref, "config C, 5000 bounces")
 
 
 def test_auto_variant_packed_state_limits(rt2mod, oraclemod, config_scene, torch_cuda):
