@@ -75,8 +75,8 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, MfmaK16Pac
             const float vz = m.z * sc.sigma;
             const _Float16 hz = (_Float16)vz;
             const _Float16 lz = (_Float16)(vz - (float)hz);
-            zhi = wave_max(fabsf((float)hz));
-            zlo = wave_max(fabsf((float)lz));
+            zhi = wave_max_s<S>(fabsf((float)hz));
+            zlo = wave_max_s<S>(fabsf((float)lz));
             write_y(bestK);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();

@@ -70,6 +70,7 @@ struct MfmaSpec {
                             // 3 = 1 without the fence between the blocks; 4 = 3 without the fence at the group end
     bool pipe = false;      // (removed: the software-pipelined k16 sweep, DESIGN.md "Tried and measured")
     int tile_groups = 0;    // k5 (render_mfma_k5t, rt2_k5_tiles.h): 32-triangle groups per LDS record tile
+    bool dpp = false;       // the per-segment wave maxima by DPP lane moves (wave_max_dpp) instead of ds_bpermute
     int sol = 0;            // speed-of-light probes (WRONG images; diag clocks only): 1 = every group reads group
                             // 0's records, 2 = no exact phase, 3 = 2 + only the U term is reduced; marginal-cost
                             // probes (same image): 4 = exact phase twice, 5 = products and reduction twice,
@@ -213,6 +214,34 @@ __device__ __forceinline__ float wave_max(float x) {
     for (int off = 32; off > 0; off >>= 1) x = fmaxf(x, __shfl_xor(x, off));
     return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
 }
+// The same maximum through DPP lane moves (no LDS crossbar round trips):
+// quad swaps, half-row and row mirrors leave every lane of a 16-lane row with
+// the row's maximum; row_bcast:15 / :31 fold rows 0-1 and 2-3 and then the
+// halves into row 3, whose lane 63 is read.  Exact (a maximum of the same
+// values in another order); x must not be NaN (the callers' values are
+// finite, or range-checked before).
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_max_step(float x) {
+    // rows outside ROW_MASK keep `old` = x: max(x, x) = x
+    const int y = __builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), CTRL, ROW_MASK, 0xf, false);
+    return fmaxf(x, __int_as_float(y));
+}
+__device__ __forceinline__ float wave_max_dpp(float x) {
+    x = dpp_max_step<0xB1, 0xf>(x);   // quad_perm [1,0,3,2]
+    x = dpp_max_step<0x4E, 0xf>(x);   // quad_perm [2,3,0,1]
+    x = dpp_max_step<0x141, 0xf>(x);  // row_half_mirror
+    x = dpp_max_step<0x140, 0xf>(x);  // row_mirror
+    x = dpp_max_step<0x142, 0xa>(x);  // row_bcast:15 into rows 1, 3
+    x = dpp_max_step<0x143, 0xc>(x);  // row_bcast:31 into rows 2, 3
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
+}
+template <MfmaSpec S>
+__device__ __forceinline__ float wave_max_s(float x) {
+    if constexpr (S.dpp)
+        return wave_max_dpp(x);
+    else
+        return wave_max(x);
+}
 
 __device__ __forceinline__ float abs_max3(const f3& v) { return fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fabsf(v.z)); }
 
@@ -228,9 +257,9 @@ struct MfmaScale {
 template <MfmaSpec S>
 __device__ __forceinline__ bool mfma_scale(float mfma_A, const f3& o, const f3& d, const f3& m, MfmaScale& sc) {
     if (__ballot(!(abs_max3(o) <= 0x1p20f && abs_max3(d) <= 1.0001f))) return false;  // NaN fails too
-    const float Omax = wave_max(abs_max3(o));
+    const float Omax = wave_max_s<S>(abs_max3(o));
     const float R0 = Omax + mfma_A + 1.0f;
-    float mx = fmaxf(fmaxf(Omax, wave_max(abs_max3(m))), 1.0f);
+    float mx = fmaxf(fmaxf(Omax, wave_max_s<S>(abs_max3(m))), 1.0f);
     if constexpr (S.ymma) mx = fmaxf(mx, __builtin_fmaf(2.25f, R0, Omax));  // |o + bk d| for every bk <= Bmax
     int ex;
     (void)frexpf(mx, &ex);
@@ -621,8 +650,8 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, SH& sh, const f
         const float vz = m.z * sc.sigma;
         const _Float16 hz = (_Float16)vz;
         const _Float16 lz = (_Float16)(vz - (float)hz);
-        zhi = wave_max(fabsf((float)hz));
-        zlo = wave_max(fabsf((float)lz));
+        zhi = wave_max_s<S>(fabsf((float)hz));
+        zlo = wave_max_s<S>(fabsf((float)lz));
     }
     auto write_y = [&](float bkv) {
         _Float16 s[16];
