@@ -564,13 +564,13 @@ def main():
         "cpu_baseline": None,
     }
     gpu_imgs = {args.traversal: img.cpu().numpy() if img is not None else None}
+    img_main = img.clone() if img is not None else None  # the headline image (renderer.image is reused below)
     gpu_values = {args.traversal: value}
     alt = "bvh" if args.traversal == "brute" else "brute"
     # brute force over 100k+ triangles takes minutes per step: not timed beside BVH there
     if world == 1 and not args.no_alt and (alt == "bvh" or sd.num_triangles <= 20000):
         # the other closest-hit algorithm on the same workload, same timing
         # bracket (reported beside the headline, never as `value`)
-        img_main = img.clone()
         scene.set_traversal(alt)
         scene.set_variant(0)
         renderer.accum.zero_()
@@ -602,7 +602,6 @@ def main():
         # reference's 53-FLOP Moller-Trumbore per pair on the FP32 VALU, no
         # MFMA (render_smem forced) — its VALU roofline is the physical one
         # for that kernel; same workload, same bracket, never `value`
-        img_main = img.clone()
         scene.set_variant(SCALAR_VARIANT)
         renderer.accum.zero_()
         scene.render(u, 0, spec.frames, renderer.sh, renderer.accum.data_ptr(), 0, stream.cuda_stream)
