@@ -10,6 +10,8 @@
 #   SVARIANTS=a,b      rank-slab probe of config B (scripts/shard_probe.py)
 #   BENCH=1            python bench.py (BENCH_ARGS)
 #   AB_LIB=exp         the A/B stages load the experiment build (rt2/librt2_exp.so)
+#   SHARD_D=v          rank-slab probe of config D (4K, 1,024 spp) with variant v (0 = automatic)
+#   STATS=1            rocprofv3 --kernel-trace --stats of the default bench workload
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
@@ -36,6 +38,14 @@ if [ -n "${CFULL}" ]; then
 fi
 if [ -n "${SVARIANTS}" ]; then
   timeout -k 10 300 python scripts/shard_probe.py --variants ${SVARIANTS} > gpurun_out/shard_ab.log 2>&1 || { echo "shard probe failed"; tail -20 gpurun_out/shard_ab.log; exit 1; }
+fi
+if [ -n "${SHARD_D}" ]; then
+  timeout -k 10 400 python scripts/shard_probe.py --config D --reps 1 --variants ${SHARD_D} > gpurun_out/shard_probe_D.log 2>&1 || { echo "shard probe D failed"; tail -20 gpurun_out/shard_probe_D.log; exit 1; }
+fi
+if [ -n "${STATS}" ]; then
+  # rocprofv3 kernel-trace summary of the default bench workload (config B)
+  export TMPDIR=/tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/stats -o run -- python3 bench.py --no-cpu-baseline --no-alt --no-config-c --no-config-e --no-scalar --steps 5 --warmup 2 > gpurun_out/stats_bench.log 2>&1 || { echo "rocprof stats failed"; tail -20 gpurun_out/stats_bench.log; exit 1; }
 fi
 if [ -n "${BENCH}" ]; then
   timeout -k 10 600 python bench.py ${BENCH_ARGS} > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail -20 gpurun_out/bench.err; exit 1; }
