@@ -7,6 +7,7 @@
 #   CVARIANTS=a,b      A/B on a config C sample (480x270, 2 frames)
 #   CFULL=a,b          A/B on the full config C step (1920x1080, 256 spp), 1 round
 #   EVARIANTS=a,b      A/B on a config E sample (480x270, 4 spp)
+#   EFULL=a,b          A/B on the full config E step (1920x1080, 4 spp), 1 round
 #   SVARIANTS=a,b      rank-slab probe of config B (scripts/shard_probe.py)
 #   BENCH=1            python bench.py (BENCH_ARGS)
 #   AB_LIB=exp         the A/B stages load the experiment build (rt2/librt2_exp.so)
@@ -32,6 +33,9 @@ if [ -n "${CVARIANTS}" ]; then
 fi
 if [ -n "${EVARIANTS}" ]; then
   RT2_LIB=${AB_LIB:-$RT2_LIB} timeout -k 10 400 python scripts/ab_variants.py --config E --width 480 --height 270 --rays 4 --variants ${EVARIANTS} --rounds 2 > gpurun_out/ab_E.json 2>&1 || { echo "ab E failed"; tail -20 gpurun_out/ab_E.json; exit 1; }
+fi
+if [ -n "${EFULL}" ]; then
+  RT2_LIB=${AB_LIB:-$RT2_LIB} timeout -k 10 400 python scripts/ab_variants.py --config E --variants ${EFULL} --rounds 1 > gpurun_out/ab_Efull.json 2>&1 || { echo "ab E full failed"; tail -20 gpurun_out/ab_Efull.json; exit 1; }
 fi
 if [ -n "${CFULL}" ]; then
   RT2_LIB=${AB_LIB:-$RT2_LIB} timeout -k 10 500 python scripts/ab_variants.py --config C --variants ${CFULL} --rounds 1 > gpurun_out/ab_Cfull.json 2>&1 || { echo "ab C full failed"; tail -20 gpurun_out/ab_Cfull.json; exit 1; }
