@@ -132,12 +132,30 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, MfmaK16Pac
         if (t + 1 < nt) issue(t + 1);
         if (!compute) continue;
         const int b = t & 1, gn = min(K, ng - t * K);
+        // a group's operands from the tile; MfmaSpec::prefetch: the next
+        // group's are read (into a second register set) before this group's
+        // products, so the LDS latency overlaps them
+        h8 nb[4];
+        float ntau = 0.0f;
+        float2 nbnd = make_float2(0.0f, 0.0f);
+        auto lds_fetch = [&](int gi) {
+            const h8* tb = &tl.rec[b][gi * 4 * 64 + lane];
+            nb[0] = tb[0];
+            nb[1] = tb[64];
+            nb[2] = tb[128];
+            nb[3] = tb[192];
+            ntau = tl.tau[b][gi * 32 + r32];
+            nbnd = tl.bnd[b][gi * 32 + r32];
+        };
+        if constexpr (S.prefetch) lds_fetch(0);
         for (int gi = 0; gi < gn; gi++) {
             const int G = t * K + gi;
-            const h8* tb = &tl.rec[b][gi * 4 * 64 + lane];
-            const h8 b0 = tb[0], b2 = tb[64], b4 = tb[128], b6 = tb[192];
-            const float tau = tl.tau[b][gi * 32 + r32];
-            const float2 bnd = tl.bnd[b][gi * 32 + r32];
+            if constexpr (!S.prefetch) lds_fetch(gi);
+            const h8 b0 = nb[0], b2 = nb[1], b4 = nb[2], b6 = nb[3];
+            const float tau = ntau;
+            const float2 bnd = nbnd;
+            if constexpr (S.prefetch)
+                if (gi + 1 < gn) lds_fetch(gi + 1);
             // sweep_k16's threshold: tau T + the bound of the left-out m.z
             // slots, padded by 2^-10 for its own rounding ("The
             // 5-product form")

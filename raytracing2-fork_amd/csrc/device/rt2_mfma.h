@@ -71,6 +71,8 @@ struct MfmaSpec {
     bool pipe = false;      // (removed: the software-pipelined k16 sweep, DESIGN.md "Tried and measured")
     int tile_groups = 0;    // k5 (render_mfma_k5t, rt2_k5_tiles.h): 32-triangle groups per LDS record tile
     bool dpp = false;       // the per-segment wave maxima by DPP lane moves (wave_max_dpp) instead of ds_bpermute
+    bool rows80 = false;    // no_tn: 80-B fragment rows, main slots 0..15 (the first K-half) + the Y slots at 16..31
+    bool wg_pool = false;   // render_mfma_pool (rt2_k5_pool.h): the workgroup's rays packed into 32-ray blocks
     int sol = 0;            // speed-of-light probes (WRONG images; diag clocks only): 1 = every group reads group
                             // 0's records, 2 = no exact phase, 3 = 2 + only the U term is reduced; marginal-cost
                             // probes (same image): 4 = exact phase twice, 5 = products and reduction twice,
@@ -291,6 +293,25 @@ __device__ __forceinline__ void mfma_main_row(_Float16* row, const f3& d, const 
     for (int k = 0; k < 4; k++)
         r[k] = h8{s[8 * k], s[8 * k + 1], s[8 * k + 2], s[8 * k + 3], s[8 * k + 4], s[8 * k + 5], s[8 * k + 6],
                   s[8 * k + 7]};
+}
+
+// mfma_main_row's first K-half only (slots 0..15: d, m.x, m.y, m.z hi), the
+// whole main fragment the forms without -tn read (MfmaSpec::rows80)
+__device__ __forceinline__ void mfma_main_row_half(_Float16* row, const f3& d, const f3& m, float sigma) {
+    const float comp[6] = {d.x, d.y, d.z, m.x, m.y, m.z};
+    _Float16 s[18];
+#pragma unroll
+    for (int c = 0; c < 6; c++) {
+        const float v = comp[c] * sigma;
+        const _Float16 hi = (_Float16)v;
+        const _Float16 lo = (_Float16)(v - (float)hi);
+        s[3 * c] = hi;
+        s[3 * c + 1] = lo;
+        s[3 * c + 2] = hi;
+    }
+    h8* r = reinterpret_cast<h8*>(row);
+    r[0] = h8{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7]};
+    r[1] = h8{s[8], s[9], s[10], s[11], s[12], s[13], s[14], s[15]};
 }
 
 // The Y fragment's k-slots 16..31 for this lane's distance bound bkv: w = o +
@@ -640,7 +661,12 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, SH& sh, const f
     const f3 m = cross(d, o);
     MfmaScale sc;
     if (!mfma_scale<S>(p.mfma_A, o, d, m, sc)) return false;
-    mfma_main_row(&sh.ray[lane][0], d, m, o, sc.sigma);
+    static_assert(!S.rows80 || (S.k5 && S.no_tn), "80-B rows hold the first K-half of the main fragment only");
+    constexpr int YO = S.rows80 ? 16 : 32;  // the Y slots' offset in a row
+    if constexpr (S.rows80)
+        mfma_main_row_half(&sh.ray[lane][0], d, m, sc.sigma);
+    else
+        mfma_main_row(&sh.ray[lane][0], d, m, o, sc.sigma);
     // k5: the wave's largest |ray lo| and |ray hi| of m.z (slots 16 and 17 of
     // the main fragment, the same arithmetic as mfma_main_row): with the
     // records' per-triangle |hi|, |lo| of the m.z coefficients they bound the
@@ -656,7 +682,7 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, SH& sh, const f
     auto write_y = [&](float bkv) {
         _Float16 s[16];
         mfma_y_chunk(s, d, o, bkv, sc.sigma, sc.Bmax);
-        h8* row = reinterpret_cast<h8*>(&sh.ray[lane][32]);
+        h8* row = reinterpret_cast<h8*>(&sh.ray[lane][YO]);
         row[0] = h8{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7]};
         row[1] = h8{s[8], s[9], s[10], s[11], s[12], s[13], s[14], s[15]};
     };
@@ -669,12 +695,12 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, SH& sh, const f
 #pragma unroll
         for (int R = 0; R < 2; R++) {
             a0[R] = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][8 * hl]);
-            a1[R] = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][16 + 8 * hl]);
+            if constexpr (!S.rows80) a1[R] = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][16 + 8 * hl]);
         }
     };
     auto read_y = [&]() {
 #pragma unroll
-        for (int R = 0; R < 2; R++) y1[R] = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][32 + 8 * hl]);
+        for (int R = 0; R < 2; R++) y1[R] = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][YO + 8 * hl]);
     };
     if constexpr (!S.afrag_lds) read_a();
     read_y();

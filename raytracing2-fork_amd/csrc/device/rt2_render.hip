@@ -39,6 +39,7 @@ using namespace rt2d;
 #include "rt2_brute.h"
 #include "rt2_mfma.h"
 #include "rt2_k5_tiles.h"
+#include "rt2_k5_pool.h"
 #include "rt2_assist.h"
 #include "rt2_bvh.h"
 #include "rt2_misc_kernels.h"
@@ -688,6 +689,10 @@ const Variant kVariants[] = {
     RT2_VARIANT(255, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(4, true, 0); x.dpp = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile4/coop0/w3/llds2/cmp/dpp"),
     RT2_VARIANT(256, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(8, true, 0); x.block = 512; x.waves = 2; return x; }()>, 512, "mfmat5/512/k5/notn/tile8/coop0/w2/llds2/cmp"),
     RT2_VARIANT(257, K_MFMA, render_mfma_k5t<k5_tiles_spec(4, true, 4)>, 768, "mfmat5/768/k5/notn/tile4/coop4/w3/llds2/cmp"),
+    RT2_VARIANT(258, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(4, true, 0); x.prefetch = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile4/coop0/w3/llds2/cmp/pf"),
+    RT2_VARIANT(259, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(4, true, 0); x.prefetch = true; x.dpp = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile4/coop0/w3/llds2/cmp/pf/dpp"),
+    RT2_VARIANT(245, K_MFMA, render_mfma_pool<[] { MfmaSpec x = kMfmaK5NoTnW4C4; x.rows80 = true; x.wg_pool = true; return x; }()>, 256, "mfmap/256/k5/notn/coop4/w4/llds2/rows80/pool"),
+    RT2_VARIANT(246, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4C4; x.rows80 = true; return x; }()>, 256, "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp/rows80"),
     RT2_VARIANT(251, K_MFMA, render_mfma_k5t<k5_tiles_spec(4, false, 0, true)>, 768, "mfmat5/768/k5/tile4/coop0/w3/llds2/cmp/diag"),
     RT2_VARIANT(253, K_MFMA, render_mfma_k5t<k5_tiles_spec(2, false, 0)>, 768, "mfmat5/768/k5/tile2/coop0/w3/llds2/cmp"),
     RT2_VARIANT(254, K_MFMA, render_mfma_k5t<k5_tiles_spec(4, false, 8)>, 768, "mfmat5/768/k5/tile4/coop8/w3/llds2/cmp"),
