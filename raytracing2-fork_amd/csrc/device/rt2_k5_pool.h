@@ -74,13 +74,18 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
             if (k < wave) base += c;
         }
         vote_parity ^= 1u;
+        // wave-uniform (LDS reads land in VGPRs): scalar registers
+        total = __builtin_amdgcn_readfirstlane(total);
+        blocks = __builtin_amdgcn_readfirstlane(blocks);
+        base = __builtin_amdgcn_readfirstlane(base);
         if (total == 0) break;  // workgroup-uniform: every wave leaves together
         const bool mine = L.st == ST_TRACE;
         // pooled when packing saves a block (the cooperative drain then has
         // nothing to do: every live ray of the workgroup is in the pool)
         const bool pooled = total <= (uint32_t)kPoolRays && ((total + 31u) >> 5) < blocks;
         const uint32_t l = lane_id();
-        uint32_t slot = 0, nb = 0;
+        uint32_t slot = 0, nb = 0, nblk = 1, nrange = 1, res = 0;
+        int G0 = 0, G1 = -1;
         bool sweeping, upper = true;
         if (pooled) {
             slot = base + lanes_below(act);
@@ -94,12 +99,24 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
                 od[5] = L.d.z;
             }
             __syncthreads();  // the pool is complete
-            // wave w sweeps packed rays 32w .. 32w+31 (lanes 32..63 and the
-            // lanes past the last ray carry a copy of the block's first ray)
-            const uint32_t j0 = 32u * (uint32_t)wave;
-            sweeping = j0 < total;
+            // wave w sweeps block b = w mod nblk (packed rays 32b .. 32b+31;
+            // lanes 32..63 and the lanes past the last ray carry a copy of the
+            // block's first ray); MfmaSpec::wg_split: with fewer blocks than
+            // waves, the NW / nblk waves of a block split its triangle groups
+            // into ranges (q = w / nblk) and the owners take the lexicographic
+            // (distance, index) minimum over the ranges — the sequential scan's
+            // result, as in coop_closest
+            nblk = (total + 31u) >> 5;
+            nrange = S.wg_split ? (uint32_t)NW / nblk : 1u;
+            const uint32_t b = (uint32_t)wave % nblk, q = (uint32_t)wave / nblk;
+            const uint32_t j0 = 32u * b;
+            sweeping = q < nrange;
             upper = false;
             if (sweeping) {
+                const int ng = (p.n_tris + 31) >> 5;
+                G0 = (int)((uint32_t)ng * q / nrange);
+                G1 = (int)((uint32_t)ng * (q + 1u) / nrange);
+                res = q * 32u * nblk + j0;
                 nb = min(32u, total - j0);
                 const uint32_t j = j0 + (l < nb ? l : 0u);
                 L.o = mk(pool.od[j][0], pool.od[j][1], pool.od[j][2]);
@@ -148,7 +165,7 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
             float bestK = 1e38f * 1.0009765625f;
             lane_stash_packed(L, sh.lane, (int)l);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            const bool swept = sweep_k16<S>(p, sh, ro, rd, best, bi, bestK, dg, upper);
+            const bool swept = sweep_k16<S>(p, sh, ro, rd, best, bi, bestK, dg, upper, G0, G1);
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             lane_unstash_packed(L, sh.lane, (int)l);
             L.o = ro;
@@ -157,8 +174,8 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
         }
         if (pooled) {
             if (sweeping && l < nb) {
-                pool.best[32u * (uint32_t)wave + l] = best;
-                pool.bi[32u * (uint32_t)wave + l] = bi;
+                pool.best[res + l] = best;
+                pool.bi[res + l] = bi;
             }
             __syncthreads();  // every block's results are in the pool
             if (mine) {
@@ -167,6 +184,14 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
                 L.d = mk(pool.od[slot][3], pool.od[slot][4], pool.od[slot][5]);
                 best = pool.best[slot];
                 bi = pool.bi[slot];
+                for (uint32_t q = 1; q < nrange; q++) {
+                    const float ob = pool.best[q * 32u * nblk + slot];
+                    const int oi = pool.bi[q * 32u * nblk + slot];
+                    if (ob < best || (ob == best && oi >= 0 && (bi < 0 || oi < bi))) {
+                        best = ob;
+                        bi = oi;
+                    }
+                }
             }
         }
         if (L.st == ST_TRACE) {

@@ -73,6 +73,7 @@ struct MfmaSpec {
     bool dpp = false;       // the per-segment wave maxima by DPP lane moves (wave_max_dpp) instead of ds_bpermute
     bool rows80 = false;    // no_tn: 80-B fragment rows, main slots 0..15 (the first K-half) + the Y slots at 16..31
     bool wg_pool = false;   // render_mfma_pool (rt2_k5_pool.h): the workgroup's rays packed into 32-ray blocks
+    bool wg_split = false;  // ... and with <= 2 blocks, each block's sweep split over the waves by triangle range
     int sol = 0;            // speed-of-light probes (WRONG images; diag clocks only): 1 = every group reads group
                             // 0's records, 2 = no exact phase, 3 = 2 + only the U term is reduced; marginal-cost
                             // probes (same image): 4 = exact phase twice, 5 = products and reduction twice,
@@ -650,7 +651,10 @@ __device__ __forceinline__ K16Terms k16_terms(const h8& a0, const h8& a1, const 
 __device__ __forceinline__ f16v Y_unused_init() { return f16v{}; }
 template <MfmaSpec S, class SH>
 __device__ __forceinline__ bool sweep_k16(const RenderParams& p, SH& sh, const f3& o, const f3& d, float& best,
-                                          int& bi, float& bestK, MfmaDiag& dg, bool upper = true) {
+                                          int& bi, float& bestK, MfmaDiag& dg, bool upper = true, int G0 = 0,
+                                          int G1 = -1) {
+    // [G0, G1): the 32-triangle groups to sweep (all of them by default; a
+    // range when several waves split one block's sweep: render_mfma_pool)
     // upper = false: lanes 32..63 carry no ray of their own (MfmaSpec::compact moved the live rays to the
     // low half), so the second 32-ray block's products and reduction are skipped
     static_assert(S.ymma && S.imax && S.minred, "the k16 sweep implements the ymma / imax / minred form");
@@ -705,13 +709,13 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, SH& sh, const f
     if constexpr (!S.afrag_lds) read_a();
     read_y();
 
-    const int ng = (p.n_tris + 31) >> 5;
-    const h8* fg = reinterpret_cast<const h8*>(p.mfma_k16_frag) + lane;
-    const float* tg = p.mfma_k16_tau + r32;
+    const int ng = G1 < 0 ? (p.n_tris + 31) >> 5 : G1;
+    const h8* fg = reinterpret_cast<const h8*>(p.mfma_k16_frag) + (size_t)G0 * (kK16Ops * 64) + lane;
+    const float* tg = p.mfma_k16_tau + 32 * G0 + r32;
     h8 b[kK16Ops], nb[kK16Ops];
     float tau = 0.0f, ntau = 0.0f;
     [[maybe_unused]] float2 bnd = make_float2(0.0f, 0.0f);
-    [[maybe_unused]] const float2* bg = p.mfma_k16_bnd + r32;
+    [[maybe_unused]] const float2* bg = p.mfma_k16_bnd + 32 * G0 + r32;
     auto fetch = [&](h8* dst, float& t) {
 #pragma unroll
         for (int op = 0; op < kK16Ops; op++)
@@ -726,7 +730,7 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, SH& sh, const f
     };
     if constexpr (S.prefetch) fetch(nb, ntau);
     if constexpr (S.lateload) fetch(b, tau);
-    for (int G = 0; G < ng; G++) {
+    for (int G = G0; G < ng; G++) {
         if constexpr (S.lateload) {
             // b, tau arrived during the previous group (requested right after
             // its last product was issued)

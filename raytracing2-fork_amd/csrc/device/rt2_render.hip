@@ -692,6 +692,8 @@ const Variant kVariants[] = {
     RT2_VARIANT(258, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(4, true, 0); x.prefetch = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile4/coop0/w3/llds2/cmp/pf"),
     RT2_VARIANT(259, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(4, true, 0); x.prefetch = true; x.dpp = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile4/coop0/w3/llds2/cmp/pf/dpp"),
     RT2_VARIANT(245, K_MFMA, render_mfma_pool<[] { MfmaSpec x = kMfmaK5NoTnW4C4; x.rows80 = true; x.wg_pool = true; return x; }()>, 256, "mfmap/256/k5/notn/coop4/w4/llds2/rows80/pool"),
+    RT2_VARIANT(247, K_MFMA, render_mfma_pool<[] { MfmaSpec x = kMfmaK5NoTnW4C4; x.rows80 = true; x.wg_pool = true; x.wg_split = true; return x; }()>, 256, "mfmap/256/k5/notn/coop4/w4/llds2/rows80/pool/split"),
+    RT2_VARIANT(248, K_MFMA, render_mfma_pool<[] { MfmaSpec x = kMfmaK5NoTnW4C4; x.rows80 = true; x.wg_pool = true; x.wg_split = true; x.tail_lanes = 0; return x; }()>, 256, "mfmap/256/k5/notn/coop0/w4/llds2/rows80/pool/split"),
     RT2_VARIANT(246, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4C4; x.rows80 = true; return x; }()>, 256, "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp/rows80"),
     RT2_VARIANT(251, K_MFMA, render_mfma_k5t<k5_tiles_spec(4, false, 0, true)>, 768, "mfmat5/768/k5/tile4/coop0/w3/llds2/cmp/diag"),
     RT2_VARIANT(253, K_MFMA, render_mfma_k5t<k5_tiles_spec(2, false, 0)>, 768, "mfmat5/768/k5/tile2/coop0/w3/llds2/cmp"),
