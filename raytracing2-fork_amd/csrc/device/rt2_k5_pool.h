@@ -29,11 +29,6 @@
 
 namespace {
 
-struct MfmaK5nLds {
-    _Float16 ray[64][40];  // 80-B rows: slots 0..15 main (first K-half), 16..31 Y (its second half)
-    uint32_t lane[15][64];
-};
-
 constexpr int kPoolRays = 128;
 struct RayPool {
     float od[kPoolRays][6];  // o.xyz, d.xyz of packed ray j

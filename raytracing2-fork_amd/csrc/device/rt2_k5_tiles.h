@@ -30,25 +30,40 @@ namespace {
 // LDS of one workgroup's record tiles: 2 buffers x K groups x the 4 operands
 // the 5-product form reads (U0, V0, X0, T1: k16 ops 0, 2, 4, 6) as 64 lanes x
 // 16 B, the per-triangle scale tau and the m.z residual bound.
-template <int K>
+template <int K, int NB = 2>
 struct K5Tiles {
-    h8 rec[2][K * 4 * 64];
-    float tau[2][K * 32];
-    float2 bnd[2][K * 32];
+    h8 rec[NB][K * 4 * 64];
+    float tau[NB][K * 32];
+    float2 bnd[NB][K * 32];
 };
 
 __device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// wait until at most n of this wave's vector-memory operations are in flight
+// (the youngest n: the pieces of the tiles issued after the awaited one)
+__device__ __forceinline__ void wait_vm(int n) {
+    if (n <= 0)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (n == 1)
+        asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else if (n == 2)
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else
+        asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+}
 
 // Closest hit of every lane's ray over all triangles, or (sweeping = false)
 // only the workgroup's tile traffic and barriers: every wave of the workgroup
 // calls it in every segment the workgroup runs.  Returns false when the wave's
 // rays are outside the filter's range (nothing computed; wave-uniform).
-template <MfmaSpec S>
-__device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, MfmaK16PackedLds& sh, K5Tiles<S.tile_groups>& tl,
+template <MfmaSpec S, class SH>
+__device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, SH& sh, K5Tiles<S.tile_groups, S.tile_bufs>& tl,
                                                const f3& o, const f3& d, float& best, int& bi, float& bestK,
                                                MfmaDiag& dg, bool sweeping, bool upper) {
     static_assert(S.k5 && S.ymma && S.imax && S.minred && S.tile_groups > 0, "the 5-product form");
-    constexpr int K = S.tile_groups, NW = S.block / 64;
+    static_assert(!S.rows80 || S.no_tn, "80-B rows hold the first K-half of the main fragment only");
+    static_assert(S.tile_bufs >= 2 && S.tile_bufs <= 3, "double or triple buffering");
+    constexpr int K = S.tile_groups, NW = S.block / 64, NB = S.tile_bufs;
+    constexpr int YO = S.rows80 ? 16 : 32;  // the Y slots' offset in a row
     const int lane = (int)lane_id();
     const int r32 = lane & 31, hl = lane >> 5, wave = (int)(threadIdx.x >> 6);
     MfmaScale sc{0.0f, 0.0f, 0.0f};
@@ -58,19 +73,22 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, MfmaK16Pac
     auto write_y = [&](float bkv) {
         _Float16 s[16];
         mfma_y_chunk(s, d, o, bkv, sc.sigma, sc.Bmax);
-        h8* row = reinterpret_cast<h8*>(&sh.ray[lane][32]);
+        h8* row = reinterpret_cast<h8*>(&sh.ray[lane][YO]);
         row[0] = h8{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7]};
         row[1] = h8{s[8], s[9], s[10], s[11], s[12], s[13], s[14], s[15]};
     };
     auto read_y = [&]() {
 #pragma unroll
-        for (int R = 0; R < 2; R++) y1[R] = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][32 + 8 * hl]);
+        for (int R = 0; R < 2; R++) y1[R] = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][YO + 8 * hl]);
     };
     if (sweeping) {
         const f3 m = cross(d, o);
         in_range = mfma_scale<S>(p.mfma_A, o, d, m, sc);
         if (in_range) {
-            mfma_main_row(&sh.ray[lane][0], d, m, o, sc.sigma);
+            if constexpr (S.rows80)
+                mfma_main_row_half(&sh.ray[lane][0], d, m, sc.sigma);
+            else
+                mfma_main_row(&sh.ray[lane][0], d, m, o, sc.sigma);
             // the wave's largest |ray lo| and |ray hi| of m.z (sweep_k16's k5 bound)
             const float vz = m.z * sc.sigma;
             const _Float16 hz = (_Float16)vz;
@@ -92,14 +110,14 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, MfmaK16Pac
     }
     const int ng = (p.n_tris + 31) >> 5, nt = (ng + K - 1) / K;
     const h8* gsrc = reinterpret_cast<const h8*>(p.mfma_k16_frag);
-    // LDS-DMA of tile t into buffer t & 1, round-robin over the waves: 4 record
+    // LDS-DMA of tile t into buffer t % NB, round-robin over the waves: 4 record
     // pieces per group (1 KiB each: a lane's 16 B land at base + 16 lane),
     // then the groups' bounds (256 B per group) and scales (128 B per group)
     // as 16-B pieces with the lanes past the tile's end masked off
     auto issue = [&](int t) {
         const int g0 = t * K, gn = min(K, ng - g0);
         const int nrec = gn * 4, nbnd = (gn * 16 + 63) / 64, ntau = (gn * 8 + 63) / 64;
-        const int b = t & 1;
+        const int b = t % NB;
         for (int pc = wave; pc < nrec + nbnd + ntau; pc += NW) {
             if (pc < nrec) {
                 const int gi = pc >> 2, op = 2 * (pc & 3);
@@ -125,13 +143,24 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, MfmaK16Pac
             }
         }
     };
-    if (nt > 0) issue(0);
+    // this wave's pieces of tile t (issued round-robin: pc = wave, wave + NW, ...)
+    auto my_pieces = [&](int t) {
+        const int gn = min(K, ng - t * K);
+        const int n = gn * 4 + (gn * 16 + 63) / 64 + (gn * 8 + 63) / 64;
+        return wave < n ? (n - wave + NW - 1) / NW : 0;
+    };
+    for (int t = 0; t < NB - 1 && t < nt; t++) issue(t);
     for (int t = 0; t < nt; t++) {
-        wait_vm0();       // this wave's pieces of tile t have landed
-        __syncthreads();  // every wave's have; every wave is done with buffer (t + 1) & 1 (tile t - 1)
-        if (t + 1 < nt) issue(t + 1);
+        // this wave's pieces of tile t have landed (the tiles issued after it
+        // may still be in flight: NB = 3 keeps tile t + 1's)
+        if constexpr (NB == 2)
+            wait_vm0();
+        else
+            wait_vm(t + 1 < nt ? my_pieces(t + 1) : 0);
+        __syncthreads();  // every wave's have; every wave is done with buffer (t + NB - 1) % NB (tile t - 1)
+        if (t + NB - 1 < nt) issue(t + NB - 1);
         if (!compute) continue;
-        const int b = t & 1, gn = min(K, ng - t * K);
+        const int b = t % NB, gn = min(K, ng - t * K);
         // a group's operands from the tile; MfmaSpec::prefetch: the next
         // group's are read (into a second register set) before this group's
         // products, so the LDS latency overlaps them
@@ -230,11 +259,12 @@ template <MfmaSpec S>
 __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves))) void render_mfma_k5t(RenderParams p_arg) {
     static_assert(S.lane_lds == 2 && S.lockstep, "packed path state, lockstep segments");
     constexpr int NW = S.block / 64;
-    __shared__ MfmaK16PackedLds wl[NW];
-    __shared__ K5Tiles<S.tile_groups> tl;
+    using WL = std::conditional_t<S.rows80, MfmaK5nLds, MfmaK16PackedLds>;
+    __shared__ WL wl[NW];
+    __shared__ K5Tiles<S.tile_groups, S.tile_bufs> tl;
     __shared__ BlockVote<NW> vote;
     uint32_t vote_parity = 0;
-    MfmaK16PackedLds& sh = wl[threadIdx.x >> 6];
+    WL& sh = wl[threadIdx.x >> 6];
     Lane L;
     lane_init(L);
     MfmaDiag dg;

@@ -74,6 +74,7 @@ struct MfmaSpec {
     bool rows80 = false;    // no_tn: 80-B fragment rows, main slots 0..15 (the first K-half) + the Y slots at 16..31
     bool wg_pool = false;   // render_mfma_pool (rt2_k5_pool.h): the workgroup's rays packed into 32-ray blocks
     bool wg_split = false;  // ... and with <= 2 blocks, each block's sweep split over the waves by triangle range
+    int tile_bufs = 2;      // render_mfma_k5t: record tile buffers (3: tile t+2 in flight while t is swept)
     int sol = 0;            // speed-of-light probes (WRONG images; diag clocks only): 1 = every group reads group
                             // 0's records, 2 = no exact phase, 3 = 2 + only the U term is reduced; marginal-cost
                             // probes (same image): 4 = exact phase twice, 5 = products and reduction twice,
@@ -557,6 +558,12 @@ __device__ __forceinline__ void lane_permute(Lane& L, int to) {
 // coordinates
 struct MfmaK16PackedLds {
     _Float16 ray[64][48];  // 96-B rows (two-way bank conflicts on the per-segment fragment reads)
+    uint32_t lane[15][64];
+};
+// the same with 80-B rows (MfmaSpec::rows80, the forms without -tn): slots
+// 0..15 the main fragment's first K-half, 16..31 the Y fragment's second half
+struct MfmaK5nLds {
+    _Float16 ray[64][40];
     uint32_t lane[15][64];
 };
 __device__ __forceinline__ void lane_stash_packed(const Lane& L, uint32_t (*st)[64], int l) {
