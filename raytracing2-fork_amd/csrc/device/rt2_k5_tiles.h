@@ -257,9 +257,10 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, SH& sh, K5
 // launcher takes this kernel only when the packed fields hold the launch.
 template <MfmaSpec S>
 __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves))) void render_mfma_k5t(RenderParams p_arg) {
-    static_assert(S.lane_lds == 2 && S.lockstep, "packed path state, lockstep segments");
+    static_assert((S.lane_lds == 2 || (S.lane_lds == 0 && S.rows80)) && S.lockstep, "lockstep segments");
     constexpr int NW = S.block / 64;
-    using WL = std::conditional_t<S.rows80, MfmaK5nLds, MfmaK16PackedLds>;
+    constexpr bool stash = S.lane_lds == 2;  // the path state waits in LDS across the tile loop
+    using WL = std::conditional_t<S.rows80, std::conditional_t<stash, MfmaK5nLds, MfmaK5rLds>, MfmaK16PackedLds>;
     __shared__ WL wl[NW];
     __shared__ K5Tiles<S.tile_groups, S.tile_bufs> tl;
     __shared__ BlockVote<NW> vote;
@@ -303,11 +304,15 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
         const f3 ro = L.o, rd = L.d;
         float best = 1e38f, bestK = 1e38f * 1.0009765625f;
         int bi = -1;
-        lane_stash_packed(L, sh.lane, (int)lane_id());
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        if constexpr (stash) {
+            lane_stash_packed(L, sh.lane, (int)lane_id());
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        }
         const bool swept = sweep_k5_tiles<S>(p, sh, tl, ro, rd, best, bi, bestK, dg, sweeping, upper);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        lane_unstash_packed(L, sh.lane, (int)lane_id());
+        if constexpr (stash) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            lane_unstash_packed(L, sh.lane, (int)lane_id());
+        }
         L.o = ro;
         L.d = rd;
         if (coop) {

@@ -566,6 +566,10 @@ struct MfmaK5nLds {
     _Float16 ray[64][40];
     uint32_t lane[15][64];
 };
+// ... without the path-state stash (the path state stays in VGPRs)
+struct MfmaK5rLds {
+    _Float16 ray[64][40];
+};
 __device__ __forceinline__ void lane_stash_packed(const Lane& L, uint32_t (*st)[64], int l) {
     const uint32_t v[15] = {(uint32_t)L.st | (uint32_t)L.inside << 3 | (uint32_t)L.bounce << 4 | (uint32_t)L.ray << 16,
                             L.item, (uint32_t)L.x | (uint32_t)L.y << 16, L.frame, L.seed,

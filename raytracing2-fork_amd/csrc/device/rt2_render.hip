@@ -692,6 +692,8 @@ const Variant kVariants[] = {
     RT2_VARIANT(237, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(4, true, 0); x.rows80 = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile4/coop0/w3/llds2/cmp/rows80"),
     RT2_VARIANT(249, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(4, true, 0); x.rows80 = true; x.tile_bufs = 3; return x; }()>, 768, "mfmat5/768/k5/notn/tile4x3/coop0/w3/llds2/cmp/rows80"),
     RT2_VARIANT(238, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(6, true, 0); x.rows80 = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile6/coop0/w3/llds2/cmp/rows80"),
+    RT2_VARIANT(212, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(8, true, 0); x.rows80 = true; x.lane_lds = 0; return x; }()>, 768, "mfmat5/768/k5/notn/tile8/coop0/w3/cmp/rows80/regs"),
+    RT2_VARIANT(213, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(10, true, 0); x.rows80 = true; x.lane_lds = 0; return x; }()>, 768, "mfmat5/768/k5/notn/tile10/coop0/w3/cmp/rows80/regs"),
     RT2_VARIANT(258, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(4, true, 0); x.prefetch = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile4/coop0/w3/llds2/cmp/pf"),
     RT2_VARIANT(259, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(4, true, 0); x.prefetch = true; x.dpp = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile4/coop0/w3/llds2/cmp/pf/dpp"),
     RT2_VARIANT(245, K_MFMA, render_mfma_pool<[] { MfmaSpec x = kMfmaK5NoTnW4C4; x.rows80 = true; x.wg_pool = true; return x; }()>, 256, "mfmap/256/k5/notn/coop4/w4/llds2/rows80/pool"),
