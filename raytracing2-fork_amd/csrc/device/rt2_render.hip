@@ -669,18 +669,21 @@ const Variant kVariants[] = {
     // default brute-force kernel (DESIGN.md "The 5-product form"): the k16 sweep with U, -V, X from the first K-half,
     // the left-out m.z slots bounded in the threshold; 3 waves per SIMD, and 4 for launches with < 1.5 items per lane
     RT2_VARIANT(227, K_MFMA, render_mfma<kMfmaK5>, 256, "mfma/256/k5/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"),
-    RT2_VARIANT(228, K_MFMA, render_mfma<kMfmaK5W4>, 256, "mfma/256/k5/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
-    // scenes of <= 8,192 triangles (records L2-resident): the same without the -tn term (4 products per block;
-    // config B 195 vs 214 ms for 227, config E sample +9 %: there the term pays), 4 waves (packed path state)
-    // or 3 when the packed fields do not hold the image / rays / bounces
-    RT2_VARIANT(233, K_MFMA, render_mfma<kMfmaK5NoTnW4>, 256, "mfma/256/k5/notn/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
+    // scenes of <= 8,192 triangles (records L2-resident): the same without the -tn term (4 products per block),
+    // 4 waves (packed path state; 243), or 3 when the packed fields do not hold the image / rays / bounces (231)
     RT2_VARIANT(231, K_MFMA, render_mfma<kMfmaK5NoTn>, 256, "mfma/256/k5/notn/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"),
     RT2_VARIANT(243, K_MFMA, render_mfma<kMfmaK5NoTnW4C4>, 256, "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
-    // LDS record tiles shared by the workgroup (rt2_k5_tiles.h; DESIGN.md "LDS record tiles")
-    RT2_VARIANT(250, K_MFMA, render_mfma_k5t<k5_tiles_spec(4, false, 0)>, 768, "mfmat5/768/k5/tile4/coop0/w3/llds2/cmp"),
+    // LDS record tiles shared by the workgroup (rt2_k5_tiles.h; DESIGN.md "LDS record tiles"): 213 the default
+    // above 8,192 triangles (10-group tiles, path state in registers), 252 the first form (4-group tiles, path
+    // state parked in LDS)
+    RT2_VARIANT(213, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(10, true, 0); x.rows80 = true; x.lane_lds = 0; return x; }()>, 768, "mfmat5/768/k5/notn/tile10/coop0/w3/cmp/rows80/regs"),
     RT2_VARIANT(252, K_MFMA, render_mfma_k5t<k5_tiles_spec(4, true, 0)>, 768, "mfmat5/768/k5/notn/tile4/coop0/w3/llds2/cmp"),
 #ifdef RT2_EXPERIMENTS
-    // earlier product kernels (round 2's 16x16x32 form; round 3's k16 sweep), kept for A/B
+    // earlier product kernels (round 2's 16x16x32 form; round 3's k16 sweep and 5-product choices; round 4's
+    // first tile form with -tn), kept for A/B
+    RT2_VARIANT(228, K_MFMA, render_mfma<kMfmaK5W4>, 256, "mfma/256/k5/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
+    RT2_VARIANT(233, K_MFMA, render_mfma<kMfmaK5NoTnW4>, 256, "mfma/256/k5/notn/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
+    RT2_VARIANT(250, K_MFMA, render_mfma_k5t<k5_tiles_spec(4, false, 0)>, 768, "mfmat5/768/k5/tile4/coop0/w3/llds2/cmp"),
     RT2_VARIANT(152, K_MFMA, render_mfma<kMfmaT8Y4>, 256, "mfma/256/f16x3/coop8/w4/imax/minred/ymma/t12"),
     RT2_VARIANT(150, K_MFMA, render_mfma<kMfmaT8Y>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma/t12"),
     RT2_VARIANT(200, K_MFMA, render_mfma<kMfmaK16>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"),
@@ -693,7 +696,6 @@ const Variant kVariants[] = {
     RT2_VARIANT(249, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(4, true, 0); x.rows80 = true; x.tile_bufs = 3; return x; }()>, 768, "mfmat5/768/k5/notn/tile4x3/coop0/w3/llds2/cmp/rows80"),
     RT2_VARIANT(238, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(6, true, 0); x.rows80 = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile6/coop0/w3/llds2/cmp/rows80"),
     RT2_VARIANT(212, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(8, true, 0); x.rows80 = true; x.lane_lds = 0; return x; }()>, 768, "mfmat5/768/k5/notn/tile8/coop0/w3/cmp/rows80/regs"),
-    RT2_VARIANT(213, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(10, true, 0); x.rows80 = true; x.lane_lds = 0; return x; }()>, 768, "mfmat5/768/k5/notn/tile10/coop0/w3/cmp/rows80/regs"),
     RT2_VARIANT(258, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(4, true, 0); x.prefetch = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile4/coop0/w3/llds2/cmp/pf"),
     RT2_VARIANT(259, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(4, true, 0); x.prefetch = true; x.dpp = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile4/coop0/w3/llds2/cmp/pf/dpp"),
     RT2_VARIANT(245, K_MFMA, render_mfma_pool<[] { MfmaSpec x = kMfmaK5NoTnW4C4; x.rows80 = true; x.wg_pool = true; return x; }()>, 256, "mfmap/256/k5/notn/coop4/w4/llds2/rows80/pool"),
@@ -854,9 +856,10 @@ constexpr int kMfmaSlabMaxTris = 8192;
 constexpr int kMfmaSmall = 243;    // <= kMfmaSlabMaxTris triangles: k5 without -tn, 4 waves (packed path state),
                                    // cooperative drain at <= 4 live rays (config B 187.9 vs 192.9 ms for 233's 8)
 constexpr int kMfmaSmallW3 = 231;  // ... 3 waves, when the packed fields cannot hold the launch
-constexpr int kMfmaTiles = 252;    // larger scenes: the 5-product form without -tn with workgroup-shared LDS record
-                                   // tiles (rt2_k5_tiles.h; DESIGN.md "LDS record tiles"): config C 26.94 vs 32.51 s
-                                   // for 227, config E sample 1.56 vs 2.53 s
+constexpr int kMfmaTiles = 213;    // larger scenes: the 5-product form without -tn with workgroup-shared LDS record
+                                   // tiles of 10 groups, the path state in registers (rt2_k5_tiles.h; DESIGN.md "LDS
+                                   // record tiles"): config C 25.94 vs 26.66 s for 252's 4-group tiles and 32.5 s for
+                                   // round 3's 227
 constexpr int kMfma = 227;  // mfma/.../k5/...: the matrix-core filter on v_mfma_f32_32x32x16_f16, 5 products per
                             // 32-ray block (DESIGN.md "The 5-product form"), registers only; larger scenes whose
                             // packed path state cannot hold the launch
@@ -1119,12 +1122,12 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
             // 2.13 s for the k16 sweep)
             // Larger scenes stream their records from the MALL unless the
             // workgroup shares them: the LDS-tiled kernel (one 12-wave
-            // workgroup per CU, packed path state), without the -tn term
-            // (config C 26.94 vs 29.19 s with it; config E sample 1.56 vs
-            // 1.60 s)
+            // workgroup per CU), without the -tn term (config C 26.94 vs
+            // 29.19 s with it; config E sample 1.56 vs 1.60 s); its path state
+            // stays in registers, so it has no packed-field limits
             if (s->n_tris <= kMfmaSlabMaxTris)
                 vi = packed && find_variant(kMfmaSmall) ? kMfmaSmall : kMfmaSmallW3;
-            else if (packed && find_variant(kMfmaTiles))
+            else if (find_variant(kMfmaTiles))
                 vi = kMfmaTiles;
         } else if (vi == kDefaultBrute) {
             // scenes outside the matrix filter's range (mfma_ok = 0):

@@ -100,8 +100,7 @@ def _last_variant(rt2mod, scene):
     return rt2mod.lib().rt2_variant_name(lv.value).decode()
 
 
-AUTO_TILES = "mfmat5/768/k5/notn/tile4/coop0/w3/llds2/cmp"  # variant 252: > 8,192 triangles, LDS record tiles
-AUTO_MFMA = "mfma/256/k5/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"  # 227: > 8,192 triangles, packed fields too small
+AUTO_TILES = "mfmat5/768/k5/notn/tile10/coop0/w3/cmp/rows80/regs"  # variant 213: > 8,192 triangles, LDS record tiles
 AUTO_SMALL = "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp"  # 243: <= 8,192 triangles
 AUTO_SMALL_W3 = "mfma/256/k5/notn/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"  # 231: packed fields too small
 
@@ -110,8 +109,8 @@ def test_auto_variant_large_scene(rt2mod, oraclemod, config_scene, torch_cuda):
     """Scenes whose matrix-filter records outgrow an XCD's L2 (config C: 100k
     triangles, 12.8 MB of k5 records) run the LDS-tiled 5-product form (one
     12-wave workgroup per CU sharing each record tile), even on this small
-    image; a bounce limit the packed path state cannot hold takes the
-    register-only 3-wave build with -tn — same image either way."""
+    image; its path state stays in registers, so a bounce limit the small-scene
+    kernel's packed state cannot hold takes it too — bit-exact either way."""
     sd, spec = config_scene("C")
     u = rt2mod.offline_uniforms(64, 36, spec.bounces, 1, sd.num_triangles)
     scene = rt2mod.Scene(sd, 0)
@@ -119,7 +118,7 @@ def test_auto_variant_large_scene(rt2mod, oraclemod, config_scene, torch_cuda):
     assert _last_variant(rt2mod, scene) == AUTO_TILES
     u.maxBounceCount = 5000
     img2 = scene.render_host(u, 0, 1)
-    assert _last_variant(rt2mod, scene) == AUTO_MFMA
+    assert _last_variant(rt2mod, scene) == AUTO_TILES
     ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(0, 36, 5), 0, 1)
     assert_exact(img2[::5], ref, "config C, 5000 bounces")
 
@@ -333,11 +332,11 @@ def test_frame_split_identical(rt2mod, oraclemod, config_scene, torch_cuda, trav
 
 
 # brute-force kernel variants that change the schedule, not the arithmetic:
-# the product variants (0 = automatic, 86, 92, 227/228/231/233/243 = the matrix filter, 250/252 = its LDS-tiled
-# form, 136 = the scalar path forced) and, in an experiment build, the A/B
+# the product variants (0 = automatic, 86, 92, 227/231/243 = the matrix filter, 213/252 = its LDS-tiled form,
+# 136 = the scalar path forced) and, in an experiment build, the A/B
 # variants (masked/plk filters, resident LDS, cooperative and team tail modes,
 # split waves, the round-1 slab kernels, occupancy hints)
-BRUTE_VARIANTS = [0, 86, 92, 227, 228, 231, 233, 243, 250, 252, 136] + ([150, 152, 200, 206, 137, 138, 139, 140, 143, 144, 145, 146] if EXPERIMENTS else []) + ([22, 24, 28, 52, 64, 65, 66, 67, 68, 70, 71, 72, 73, 74, 76, 79, 80, 84, 85, 87, 89, 95, 97, 101, 104, 106,
+BRUTE_VARIANTS = [0, 86, 92, 213, 227, 231, 243, 252, 136] + ([150, 152, 200, 206, 228, 233, 250, 137, 138, 139, 140, 143, 144, 145, 146] if EXPERIMENTS else []) + ([22, 24, 28, 52, 64, 65, 66, 67, 68, 70, 71, 72, 73, 74, 76, 79, 80, 84, 85, 87, 89, 95, 97, 101, 104, 106,
                                  90] if EXPERIMENTS else [])
 
 
