@@ -69,6 +69,7 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, SH& sh, K5
     MfmaScale sc{0.0f, 0.0f, 0.0f};
     float zlo = 0.0f, zhi = 0.0f;
     h8 a0[2], a1[2], y1[2];
+    [[maybe_unused]] ThrBits thr = {};
     bool compute = false, in_range = true;
     auto write_y = [&](float bkv) {
         _Float16 s[16];
@@ -95,6 +96,7 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, SH& sh, K5
             const _Float16 lz = (_Float16)(vz - (float)hz);
             zhi = wave_max_s<S>(fabsf((float)hz));
             zlo = wave_max_s<S>(fabsf((float)lz));
+            if constexpr (S.cthr) thr = mfma_thr_bits(sc.Tw, zlo, zhi);
             write_y(bestK);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -116,7 +118,8 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, SH& sh, K5
     // as 16-B pieces with the lanes past the tile's end masked off
     auto issue = [&](int t) {
         const int g0 = t * K, gn = min(K, ng - g0);
-        const int nrec = gn * 4, nbnd = (gn * 16 + 63) / 64, ntau = (gn * 8 + 63) / 64;
+        // cthr: the -tn record carries the threshold; no bounds or scales
+        const int nrec = gn * 4, nbnd = S.cthr ? 0 : (gn * 16 + 63) / 64, ntau = S.cthr ? 0 : (gn * 8 + 63) / 64;
         const int b = t % NB;
         for (int pc = wave; pc < nrec + nbnd + ntau; pc += NW) {
             if (pc < nrec) {
@@ -146,7 +149,7 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, SH& sh, K5
     // this wave's pieces of tile t (issued round-robin: pc = wave, wave + NW, ...)
     auto my_pieces = [&](int t) {
         const int gn = min(K, ng - t * K);
-        const int n = gn * 4 + (gn * 16 + 63) / 64 + (gn * 8 + 63) / 64;
+        const int n = gn * 4 + (S.cthr ? 0 : (gn * 16 + 63) / 64 + (gn * 8 + 63) / 64);
         return wave < n ? (n - wave + NW - 1) / NW : 0;
     };
     for (int t = 0; t < NB - 1 && t < nt; t++) issue(t);
@@ -173,8 +176,10 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, SH& sh, K5
             nb[1] = tb[64];
             nb[2] = tb[128];
             nb[3] = tb[192];
-            ntau = tl.tau[b][gi * 32 + r32];
-            nbnd = tl.bnd[b][gi * 32 + r32];
+            if constexpr (!S.cthr) {
+                ntau = tl.tau[b][gi * 32 + r32];
+                nbnd = tl.bnd[b][gi * 32 + r32];
+            }
         };
         if constexpr (S.prefetch) lds_fetch(0);
         for (int gi = 0; gi < gn; gi++) {
@@ -188,6 +193,10 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, SH& sh, K5
             // sweep_k16's threshold: tau T + the bound of the left-out m.z
             // slots, padded by 2^-10 for its own rounding ("The
             // 5-product form")
+            unsigned long long M;
+            if constexpr (S.cthr) {
+                M = k5_cthr_group<S>(thr, a0, y1, b0, b2, b4, b6, upper, sh);
+            } else {
             const float Tl = tau * sc.Tw + (bnd.x * zlo + bnd.y * zhi) * 1.0009765625f;
             int tmin = 0x7fffffff;
 #pragma unroll
@@ -216,7 +225,8 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, SH& sh, K5
                 }
                 if (R == 1) __builtin_amdgcn_sched_barrier(0);
             }
-            const unsigned long long M = __ballot(tmin <= __float_as_int(Tl));
+            M = __ballot(tmin <= __float_as_int(Tl));
+            }
             if constexpr (S.diag) dg.groups += 1;
             if (M) {
                 if constexpr (S.diag) dg.hot += 1;

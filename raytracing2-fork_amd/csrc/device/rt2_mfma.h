@@ -75,6 +75,10 @@ struct MfmaSpec {
     bool wg_pool = false;   // render_mfma_pool (rt2_k5_pool.h): the workgroup's rays packed into 32-ray blocks
     bool wg_split = false;  // ... and with <= 2 blocks, each block's sweep split over the waves by triangle range
     int tile_bufs = 2;      // render_mfma_k5t: record tile buffers (3: tile t+2 in flight while t is swept)
+    bool ylds = false;      // cthr: each block's main and Y fragments are read from LDS right before its products
+    bool cthr = false;      // k5 no_tn: the threshold rides in the products' accumulator operand (one matrix
+                            // product per group, mfma_thr_frag), and the reduction is a sign-bit AND / OR
+                            // (2 v_bitop3_b32 per pair instead of 2.5 min / max)
     int sol = 0;            // speed-of-light probes (WRONG images; diag clocks only): 1 = every group reads group
                             // 0's records, 2 = no exact phase, 3 = 2 + only the U term is reduced; marginal-cost
                             // probes (same image): 4 = exact phase twice, 5 = products and reduction twice,
@@ -629,6 +633,14 @@ __global__ void prep_mfma_k16(const float4* tri, int n, int n_pad, _Float16* out
         const int q = op < 6 ? op >> 1 : 3, h = op < 6 ? (op & 1) : 1;
         _Float16 slot[32];
         mfma_slots(k.c[q], k.tau, slot);
+        if (op == 6) {
+            // the threshold slots 29..31 of the -tn record (zero in every ray
+            // fragment but mfma_thr_frag): -tau, -CH, -CL, all exact in f16
+            // (tau a power of two in [2^-9, 2^13]; CH, CL f16 magnitudes)
+            slot[29] = (_Float16)(float)-k.tau;
+            slot[30] = (_Float16)-ch;
+            slot[31] = (_Float16)-cl;
+        }
         for (int j = 0; j < 16; j++)
             out[((size_t)(G * kK16Ops + op) * 64 + t + 32 * (j >> 3)) * 8 + (j & 7)] = slot[16 * h + j];
         if (op < 6) {
@@ -638,6 +650,40 @@ __global__ void prep_mfma_k16(const float4* tri, int n, int n_pad, _Float16* out
     }
     tau_out[i] = (float)k.tau;
     if (bnd_out) bnd_out[i] = make_float2(ch, cl);
+}
+
+// f16 of v > 0 rounded up (the threshold may only grow)
+__device__ __forceinline__ _Float16 f16_up(float v) {
+    _Float16 h = (_Float16)v;
+    if ((float)h < v) h = __builtin_bit_cast(_Float16, (uint16_t)(__builtin_bit_cast(uint16_t, h) + 1u));
+    return h;
+}
+// MfmaSpec::cthr: the A fragment whose product with the -tn record's second
+// K-half is -Tl'' in every row, Tl'' = tau Tw + CH ML + CL MH with the wave's
+// factors padded by 2^-8 and rounded up to f16 (slots 29..31 against the
+// record's -tau, -CH, -CL; every other slot 0).  The three products are exact
+// in f32 and of one sign, so the sum's rounding (2^-23) is inside the pad:
+// Tl'' > Tl' = tau Tw + (CH ML + CL MH)(1 + 2^-10), sweep_k16's threshold.
+// Added as the accumulator operand, it turns "term <= Tl'" into "term' < 0";
+// DESIGN.md, "The threshold in the accumulator".  The factors are wave-uniform
+// and kept as two scalar words (elements 4, 5 = 0, Tw; 6, 7 = ML, MH of the
+// upper lanes' 8 slots); the fragment is rebuilt from them every group (two
+// v_cndmask), so its 4 VGPRs are not live across the sweep.
+struct ThrBits {
+    uint32_t w2, w3;
+};
+__device__ __forceinline__ ThrBits mfma_thr_bits(float Tw, float zlo, float zhi) {
+    constexpr float pad = 1.00390625f;  // 1 + 2^-8
+    const uint32_t t = __builtin_bit_cast(uint16_t, f16_up(Tw * pad));
+    const uint32_t a = __builtin_bit_cast(uint16_t, f16_up(zlo * pad));
+    const uint32_t b = __builtin_bit_cast(uint16_t, f16_up(zhi * pad));
+    return ThrBits{(uint32_t)__builtin_amdgcn_readfirstlane(t << 16), (uint32_t)__builtin_amdgcn_readfirstlane(a | b << 16)};
+}
+__device__ __forceinline__ h8 mfma_thr_frag(ThrBits tb) {
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    const bool up = lane_id() >= 32;  // slots 8..15 of the K-half: 29, 30, 31 are elements 5, 6, 7
+    const u4 v = {0u, 0u, up ? opaque(tb.w2) : 0u, up ? opaque(tb.w3) : 0u};
+    return __builtin_bit_cast(h8, v);
 }
 
 // The five terms of 32 rays (fragments a0/a1 = the main fragment's two
@@ -657,6 +703,48 @@ __device__ __forceinline__ K16Terms k16_terms(const h8& a0, const h8& a1, const 
     r.T = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b[6], zero, 0, 0, 0);
     r.Y = __builtin_amdgcn_mfma_f32_32x32x16_f16(y1, b[6], zero, 0, 0, 0);
     return r;
+}
+
+// MfmaSpec::cthr: one group's filter for the wave's one or two 32-ray blocks.
+// TT = -Tl'' in every row (mfma_thr_frag x the -tn record); each term is
+// computed as its sum plus TT, so a pair passes iff all four shifted terms
+// are negative: the sign bit of U & V & X & Y (two v_bitop3_b32), ORed over
+// the lane's 16 pairs (all one triangle).  The accumulation error of the 17
+// summands is inside the 31 x 2^-24 budget of the 30-product form.
+// MfmaSpec::ylds: a block's fragments are read from the wave's LDS rows right
+// before its products (no fragment live across the group: 4-wave budget).
+template <MfmaSpec S, class SH>
+__device__ __forceinline__ unsigned long long k5_cthr_group(ThrBits tb, const h8* a0, const h8* y1, const h8& b0,
+                                                            const h8& b2, const h8& b4, const h8& b6, bool upper,
+                                                            const SH& sh) {
+    static_assert(S.k5 && S.no_tn && S.sol == 0, "the 4-product form");
+    constexpr int YO = S.rows80 ? 16 : 32;
+    const int r32 = (int)lane_id() & 31, hl = (int)lane_id() >> 5;
+    const f16v zero = {};
+    const f16v TT = __builtin_amdgcn_mfma_f32_32x32x16_f16(mfma_thr_frag(tb), b6, zero, 0, 0, 0);
+    int acc = 0;
+#pragma unroll
+    for (int R = 0; R < 2; R++) {
+        if (R == 1 && !upper) break;
+        const h8 aR = S.ylds ? *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][8 * hl]) : a0[R];
+        const f16v U = __builtin_amdgcn_mfma_f32_32x32x16_f16(aR, b0, TT, 0, 0, 0);
+        const f16v V = __builtin_amdgcn_mfma_f32_32x32x16_f16(aR, b2, TT, 0, 0, 0);
+        const f16v X = __builtin_amdgcn_mfma_f32_32x32x16_f16(aR, b4, TT, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        int t3[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++)  // U & V & X (LUT index 4 S0 + 2 S1 + S2)
+            t3[i] = __builtin_amdgcn_bitop3_b32(__float_as_int(U[i]), __float_as_int(V[i]), __float_as_int(X[i]), 0x80);
+        __builtin_amdgcn_sched_barrier(0);
+        const h8 yR = S.ylds ? *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][YO + 8 * hl]) : y1[R];
+        const f16v Y = __builtin_amdgcn_mfma_f32_32x32x16_f16(yR, b6, TT, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 16; i++)  // (t3 & Y) | acc: one chain, no OR tree (which costs 0.5 more per pair)
+            acc = __builtin_amdgcn_bitop3_b32(t3[i], __float_as_int(Y[i]), acc, 0xEA);
+        if (R == 1) __builtin_amdgcn_sched_barrier(0);
+    }
+    return __ballot(acc < 0);
 }
 
 __device__ __forceinline__ f16v Y_unused_init() { return f16v{}; }
@@ -717,8 +805,10 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, SH& sh, const f
 #pragma unroll
         for (int R = 0; R < 2; R++) y1[R] = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][YO + 8 * hl]);
     };
-    if constexpr (!S.afrag_lds) read_a();
-    read_y();
+    if constexpr (!S.afrag_lds && !S.ylds) read_a();
+    if constexpr (!S.ylds) read_y();
+    [[maybe_unused]] ThrBits thr = {};
+    if constexpr (S.cthr) thr = mfma_thr_bits(sc.Tw, zlo, zhi);
 
     const int ng = G1 < 0 ? (p.n_tris + 31) >> 5 : G1;
     const h8* fg = reinterpret_cast<const h8*>(p.mfma_k16_frag) + (size_t)G0 * (kK16Ops * 64) + lane;
@@ -731,10 +821,12 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, SH& sh, const f
 #pragma unroll
         for (int op = 0; op < kK16Ops; op++)
             if (!S.k5 || !(op & 1) || op == 6) dst[op] = fg[64 * op];  // k5: the second K-halves of U V X unused
-        t = *tg;
-        if constexpr (S.k5) {
-            bnd = *bg;
-            bg += 32;
+        if constexpr (!S.cthr) {  // cthr: the -tn record carries the threshold
+            t = *tg;
+            if constexpr (S.k5) {
+                bnd = *bg;
+                bg += 32;
+            }
         }
         fg += kK16Ops * 64;
         tg += 32;
@@ -758,6 +850,10 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, SH& sh, const f
             fetch(b, tau);
         }
         if constexpr (S.afrag_lds) read_a();
+        unsigned long long M;
+        if constexpr (S.cthr) {
+            M = k5_cthr_group<S>(thr, a0, y1, b[0], b[2], b[4], b[6], upper, sh);
+        } else {
         float Tl = tau * sc.Tw;
         // k5: + |c_hi| max|ray lo| + |c_lo| max|ray hi| of the left-out m.z
         // slots, padded by 2^-10 for its own rounding ("The
@@ -880,8 +976,9 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, SH& sh, const f
             if (tmin6 == 0x12345677) best = -best;  // never (a sink)
         if constexpr (S.sol == 7)
             if (ex[0] == 1.2345e-30f) best = -best;  // never (a sink)
-        const unsigned long long M = (S.sol == 2 || S.sol == 3) ? (unsigned long long)(tmin == 0x7ffffffe)
-                                                                 : __ballot(tmin <= __float_as_int(Tl));
+        M = (S.sol == 2 || S.sol == 3) ? (unsigned long long)(tmin == 0x7ffffffe)
+                                       : __ballot(tmin <= __float_as_int(Tl));
+        }
         if constexpr (S.diag) dg.groups += 1;
         if (M) {
             if constexpr (S.diag) dg.hot += 1;
@@ -922,7 +1019,7 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, SH& sh, const f
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                read_y();
+                if constexpr (!S.ylds) read_y();
             }
         }
     }
@@ -984,6 +1081,14 @@ __global__ __launch_bounds__(64) void mfma_probe_kernel(RenderParams p, const fl
     const size_t ray0 = (size_t)blockIdx.x * 64;
     if constexpr (S.k16) {
         const int r32 = lane & 31, hl = lane >> 5;
+        // MfmaSpec::cthr: the sweep's threshold factors (the wave's m.z halves)
+        [[maybe_unused]] ThrBits tb = {};
+        if constexpr (S.cthr) {
+            const float vz = m.z * sc.sigma;
+            const _Float16 hz = (_Float16)vz;
+            const _Float16 lz = (_Float16)(vz - (float)hz);
+            tb = mfma_thr_bits(sc.Tw, wave_max(fabsf((float)lz)), wave_max(fabsf((float)hz)));
+        }
         const h8* fg = reinterpret_cast<const h8*>(p.mfma_k16_frag) + lane;
         for (int G = 0; G < n_pad / 32; G++) {
             h8 b[kK16Ops];
@@ -994,11 +1099,19 @@ __global__ __launch_bounds__(64) void mfma_probe_kernel(RenderParams p, const fl
                 const h8 y1 = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][32 + 8 * hl]);
                 K16Terms q = k16_terms(a0, a1, y1, b);
                 if constexpr (S.k5) {
-                    // the 5-product form: U, -V, X from the first K-half only
+                    // the 5-product form: U, -V, X from the first K-half only;
+                    // cthr: all four with the threshold product TT as the
+                    // accumulator (k5_cthr_group), TT itself in the -tn slot
                     const f16v zero = {};
-                    q.U = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b[0], zero, 0, 0, 0);
-                    q.V = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b[2], zero, 0, 0, 0);
-                    q.X = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b[4], zero, 0, 0, 0);
+                    f16v c = zero;
+                    if constexpr (S.cthr) c = __builtin_amdgcn_mfma_f32_32x32x16_f16(mfma_thr_frag(tb), b[6], zero, 0, 0, 0);
+                    q.U = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b[0], c, 0, 0, 0);
+                    q.V = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b[2], c, 0, 0, 0);
+                    q.X = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b[4], c, 0, 0, 0);
+                    if constexpr (S.cthr) {
+                        q.T = c;
+                        q.Y = __builtin_amdgcn_mfma_f32_32x32x16_f16(y1, b[6], c, 0, 0, 0);
+                    }
                 }
                 for (int i = 0; i < 16; i++) {
                     const size_t rr = ray0 + 32 * R + 8 * (i >> 2) + 4 * hl + (i & 3);

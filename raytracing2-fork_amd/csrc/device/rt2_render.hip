@@ -695,6 +695,12 @@ const Variant kVariants[] = {
     RT2_VARIANT(237, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(4, true, 0); x.rows80 = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile4/coop0/w3/llds2/cmp/rows80"),
     RT2_VARIANT(249, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(4, true, 0); x.rows80 = true; x.tile_bufs = 3; return x; }()>, 768, "mfmat5/768/k5/notn/tile4x3/coop0/w3/llds2/cmp/rows80"),
     RT2_VARIANT(238, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(6, true, 0); x.rows80 = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile6/coop0/w3/llds2/cmp/rows80"),
+    RT2_VARIANT(214, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(10, true, 0); x.rows80 = true; x.lane_lds = 0; x.prefetch = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile10/coop0/w3/cmp/rows80/regs/pf"),
+    RT2_VARIANT(215, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(10, true, 8); x.rows80 = true; x.lane_lds = 0; return x; }()>, 768, "mfmat5/768/k5/notn/tile10/coop8/w3/cmp/rows80/regs"),
+    RT2_VARIANT(217, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(10, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile10/coop0/w3/cmp/rows80/regs/cthr"),
+    RT2_VARIANT(260, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4C4; x.cthr = true; return x; }()>, 256, "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp/cthr"),
+    RT2_VARIANT(261, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4C4; x.cthr = true; x.ylds = true; return x; }()>, 256, "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp/cthr/ylds"),
+    RT2_VARIANT(216, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(11, true, 0); x.rows80 = true; x.lane_lds = 0; return x; }()>, 768, "mfmat5/768/k5/notn/tile11/coop0/w3/cmp/rows80/regs"),
     RT2_VARIANT(212, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(8, true, 0); x.rows80 = true; x.lane_lds = 0; return x; }()>, 768, "mfmat5/768/k5/notn/tile8/coop0/w3/cmp/rows80/regs"),
     RT2_VARIANT(258, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(4, true, 0); x.prefetch = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile4/coop0/w3/llds2/cmp/pf"),
     RT2_VARIANT(259, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(4, true, 0); x.prefetch = true; x.dpp = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile4/coop0/w3/llds2/cmp/pf/dpp"),
@@ -1436,13 +1442,15 @@ extern "C" long long rt2_scene_export(rt2_scene* s, int what, void* host, unsign
 // best, d.xyz, 0) against every triangle of the scene.  layout 0 = the
 // 16x16x32 form of render_mfma (variants 150/152), 1 = the k16 form
 // (sweep_k16), 2 = its 5-product form (MfmaSpec::k5: U, -V, X from the first
-// K-half).  Host outputs, sized by the caller: terms [n_rays][n_pad][5]
+// K-half), 3 = the 5-product form with the threshold in the accumulator
+// (MfmaSpec::cthr: U, -V, X, Y shifted by TT = -Tl'', TT in the -tn slot).
+// Host outputs, sized by the caller: terms [n_rays][n_pad][5]
 // (n_pad = triangles padded to 16 / 32), frags [n_rays][48] f16 bits, rinfo
 // [n_rays][8], accept [n_rays][n_tris].
 extern "C" int rt2_mfma_probe(rt2_scene* s, int layout, const float* rays, int32_t n_rays, float* terms,
                               uint16_t* frags, float* rinfo, uint8_t* accept) {
     if (!s || !rays || n_rays <= 0 || n_rays % 64 != 0 || !terms || !frags || !rinfo || !accept ||
-        layout < 0 || layout > 2 || s->n_tris < 1 || !s->mfma_ok) {
+        layout < 0 || layout > 3 || s->n_tris < 1 || !s->mfma_ok) {
         rt2h::set_error("rt2_mfma_probe: bad argument (n_rays a positive multiple of 64, a scene in the filter's "
                         "range)");
         return -1;
@@ -1481,7 +1489,17 @@ extern "C" int rt2_mfma_probe(rt2_scene* s, int layout, const float* rays, int32
             x.k5 = true;
             return x;
         }();
-        if (layout == 1)
+        constexpr MfmaSpec k5c = [] {
+            MfmaSpec x = k16_spec(3);
+            x.k5 = true;
+            x.no_tn = true;
+            x.cthr = true;
+            return x;
+        }();
+        if (layout == 3)
+            hipLaunchKernelGGL(mfma_probe_kernel<k5c>, dim3(n_rays / 64), dim3(64), 0, 0, p, d_rays, n_pad, d_terms,
+                               d_frags, d_info, d_acc);
+        else if (layout == 1)
             hipLaunchKernelGGL(mfma_probe_kernel<k16>, dim3(n_rays / 64), dim3(64), 0, 0, p, d_rays, n_pad, d_terms,
                                d_frags, d_info, d_acc);
         else if (layout == 2)

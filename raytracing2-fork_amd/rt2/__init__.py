@@ -596,7 +596,8 @@ class Scene:
     def mfma_probe(self, layout: int, rays: np.ndarray):
         """The matrix filter's terms on the device (rt2_mfma_probe, test hook):
         rays (n, 8) float32 {o, best, d, 0}, n a multiple of 64; layout 0 =
-        16x16x32 (render_mfma), 1 = k16, 2 = its 5-product form (k5).  Returns (terms [n, n_pad, 5], frags
+        16x16x32 (render_mfma), 1 = k16, 2 = its 5-product form (k5), 3 = k5 with the threshold in the
+        accumulator (cthr: U, -V, X, Y shifted by TT, TT in slot 3).  Returns (terms [n, n_pad, 5], frags
         [n, 48] float16, rinfo [n, 8], accept [n, n_tris] bool)."""
         rays = np.ascontiguousarray(rays, dtype=np.float32)
         n = rays.shape[0]

@@ -41,7 +41,7 @@ if [ -n "${CFULL}" ]; then
   RT2_LIB=${AB_LIB:-$RT2_LIB} timeout -k 10 500 python scripts/ab_variants.py --config C --variants ${CFULL} --rounds 1 > gpurun_out/ab_Cfull.json 2>&1 || { echo "ab C full failed"; tail -20 gpurun_out/ab_Cfull.json; exit 1; }
 fi
 if [ -n "${SVARIANTS}" ]; then
-  RT2_LIB=${AB_LIB:-$RT2_LIB} timeout -k 10 300 python scripts/shard_probe.py --variants ${SVARIANTS} > gpurun_out/shard_ab.log 2>&1 || { echo "shard probe failed"; tail -20 gpurun_out/shard_ab.log; exit 1; }
+  RT2_LIB=${AB_LIB:-$RT2_LIB} timeout -k 10 300 python scripts/shard_probe.py --reps ${SREPS:-3} --variants ${SVARIANTS} > gpurun_out/shard_ab.log 2>&1 || { echo "shard probe failed"; tail -20 gpurun_out/shard_ab.log; exit 1; }
 fi
 if [ -n "${SHARD_D}" ]; then
   timeout -k 10 400 python scripts/shard_probe.py --config D --reps 1 --variants ${SHARD_D} > gpurun_out/shard_probe_D.log 2>&1 || { echo "shard probe D failed"; tail -20 gpurun_out/shard_probe_D.log; exit 1; }

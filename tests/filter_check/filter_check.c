@@ -227,6 +227,22 @@ static int mfma_record(f3 a, f3 e0, f3 e1, f3 n, double slot[MQ][32], double* ta
  * record's largest |slot 16|, |slot 17| over U, -V, X), padded by 2^-10.  The
  * wave's maxima are at least this ray's own values; the check uses exactly
  * those (the smallest bound a wave can have). */
+/* f16 of v > 0 rounded up (rt2_mfma.h f16_up) */
+static double f16_up(float v) {
+    double h = to_f16(v);
+    if (h < v) {
+        int e;
+        (void)frexp(h, &e);
+        h += h < 0x1p-14 ? 0x1p-24 : ldexp(1.0, e - 12);  /* h in [2^(e-1), 2^e): quantum 2^(e-11) */
+    }
+    return h;
+}
+/* k5 = 2 (MfmaSpec::cthr): the same 4-term form with the threshold in the
+ * accumulator: TT = -(tau Tw'' + CH ML'' + CL MH'') from the -tn record's
+ * slots 29..31 (-tau, -CH, -CL) times mfma_thr_frag's f16 factors (padded by
+ * 2^-8, rounded up), its 3-term f32 sum moved toward zero by 2u; each term is
+ * its products plus TT, moved by 31 u (sum |p| + |TT|) toward rejection, and
+ * passes iff negative (the sign-bit AND). */
 static int pass_mfma(f3 o, f3 d, double slot[MQ][32], double tau, float As, float Ow, float Mw, float bestK,
                      int ymma, float ts, int k5) {
     const f3 m = cross(d, o);
@@ -253,7 +269,15 @@ static int pass_mfma(f3 o, f3 d, double slot[MQ][32], double tau, float As, floa
     ray[27] = ray[28] = sigma;
     ray[29] = ray[30] = ray[31] = 0.0;
     float Tl = (float)tau * Tw;
-    if (k5) {
+    double TT = 0.0;
+    if (k5 == 2) {
+        float ch = 0.0f, cl = 0.0f;
+        for (int q = 0; q < 3; q++) ch = fmaxf(ch, (float)fabs(slot[q][16])), cl = fmaxf(cl, (float)fabs(slot[q][17]));
+        const float pad = 1.00390625f;
+        const double s3 = (double)(float)tau * f16_up(Tw * pad) + (double)ch * f16_up((float)fabs(ray[16]) * pad) +
+                          (double)cl * f16_up((float)fabs(ray[17]) * pad);
+        TT = -s3 * (1.0 - 0x1p-23);
+    } else if (k5) {
         float ch = 0.0f, cl = 0.0f;
         for (int q = 0; q < 3; q++) ch = fmaxf(ch, (float)fabs(slot[q][16])), cl = fmaxf(cl, (float)fabs(slot[q][17]));
         Tl += (ch * (float)fabs(ray[16]) + cl * (float)fabs(ray[17])) * 1.0009765625f;
@@ -261,7 +285,7 @@ static int pass_mfma(f3 o, f3 d, double slot[MQ][32], double tau, float As, floa
     const float cd = (float)tau * Cw;
     float qv[MQ], qe[MQ];
     for (int q = 0; q < MQ; q++) {
-        double s = q == 4 ? cd : 0.0, sa = q == 4 ? fabs(cd) : 0.0;
+        double s = q == 4 ? cd : TT, sa = q == 4 ? fabs(cd) : fabs(TT);
         for (int k = 0; k < 32; k++) {
             if (k5 && q < 3 && (k == 16 || k == 17)) continue;  /* the products the 5-product form leaves out */
             const double p = ray[k] * slot[q][k];
@@ -288,8 +312,8 @@ static int pass_mfma(f3 o, f3 d, double slot[MQ][32], double tau, float As, floa
             yr[18 + 3 * c] = hi, yr[19 + 3 * c] = lo, yr[20 + 3 * c] = hi;
         }
         yr[27] = yr[28] = fin ? -sigma : 0.0f;
-        double sy = 0.0, sa = 0.0;
-        for (int k = 0; k < 32; k++) {
+        double sy = TT, sa = fabs(TT);
+        for (int k = 0; k < 29; k++) {  /* slots 29..31 (the cthr threshold) are 0 in this fragment */
             const double p = yr[k] * slot[3][k];
             sy += p;
             sa += fabs(p);
@@ -299,7 +323,11 @@ static int pass_mfma(f3 o, f3 d, double slot[MQ][32], double tau, float As, floa
         const float bk = bestK <= Bmax ? bestK : INFINITY;
         Y = fmaf(bk, qv[4] + qe[4], -(qv[3] - qe[3]));
     }
-    const float t = fmaxf(fmaxf(fmaxf(qv[0] + qe[0], qv[1] + qe[1]), fmaxf(qv[2] + qe[2], qv[3] + qe[3])), Y);
+    if (k5 == 2)  /* no -tn term; all four shifted terms negative */
+        return qv[0] + qe[0] < 0.0f && qv[1] + qe[1] < 0.0f && qv[2] + qe[2] < 0.0f && Y < 0.0f;
+    /* k5 = 3: the 5-product form without its -tn term (MfmaSpec::no_tn) */
+    const float tn = k5 == 3 ? -INFINITY : qv[3] + qe[3];
+    const float t = fmaxf(fmaxf(fmaxf(qv[0] + qe[0], qv[1] + qe[1]), fmaxf(qv[2] + qe[2], tn)), Y);
     return t <= Tl;
 }
 
@@ -309,7 +337,7 @@ int main(int argc, char** argv) {
     long long accepts = 0, bad_old = 0, bad_new = 0, p_old = 0, p_new = 0, bad_plk = 0, p_plk = 0, p_plk_near = 0, p_old_near = 0;
     long long bad_mfma = 0, p_mfma = 0, n_mfma = 0, p_mfma_near = 0, n_mfma_near = 0;
     long long bad_y = 0, p_y = 0, p_y_near = 0;
-    long long bad_k5 = 0, p_k5 = 0, p_k5_near = 0;
+    long long bad_k5 = 0, p_k5 = 0, p_k5_near = 0, bad_ct = 0, p_ct = 0, p_ct_near = 0, p_kn = 0, p_kn_near = 0;
     for (long long it = 0; it < n; it++) {
         const int kind = (int)(next64() % 6);
         const int far = (next64() % 4) == 0;  /* small triangle far from the origin */
@@ -385,6 +413,13 @@ int main(int argc, char** argv) {
             p_k5 += f5;
             if (ex && !f5) bad_k5++;
             if (!far && !wide && wk == 0 && inr) p_k5_near += f5;
+            const int fc = pass_mfma(o, d, slot, tau, As, Ow, Mw, bestK, 1, YMMA_TS, 2);
+            const int fk = pass_mfma(o, d, slot, tau, As, Ow, Mw, bestK, 1, YMMA_TS, 3);
+            p_kn += fk;
+            if (!far && !wide && wk == 0 && inr) p_kn_near += fk;
+            p_ct += fc;
+            if (ex && !fc) bad_ct++;
+            if (!far && !wide && wk == 0 && inr) p_ct_near += fc;
             n_mfma++;
             p_mfma += fm;
             p_y += fy;
@@ -400,9 +435,9 @@ int main(int argc, char** argv) {
         if (ex && !fo) bad_old++;
         if (ex && !fn) bad_new++;
     }
-    printf("%lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld\n", n, accepts,
-           bad_old, bad_new, p_old, p_new, bad_plk, p_plk, bad_mfma, p_mfma, n_mfma, p_mfma_near, n_mfma_near, bad_y,
-           p_y, p_y_near, bad_k5, p_k5, p_k5_near);
+    printf("%lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld\n",
+           n, accepts, bad_old, bad_new, p_old, p_new, bad_plk, p_plk, bad_mfma, p_mfma, n_mfma, p_mfma_near,
+           n_mfma_near, bad_y, p_y, p_y_near, bad_k5, p_k5, p_k5_near, bad_ct, p_ct, p_ct_near, p_kn, p_kn_near);
     fprintf(stderr, "near-origin draws: pass_old %lld pass_plk %lld\n", p_old_near, p_plk_near);
     return 0;
 }

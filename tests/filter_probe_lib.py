@@ -170,6 +170,71 @@ def analyse(terms, frags, rinfo, accept, B, coef, tau, rays, T_tau, bnd=None):
     return out, violations
 
 
+def f16_up(v):
+    """f16 of v > 0 rounded up, as float64 (rt2_mfma.h f16_up)."""
+    v = np.asarray(v, dtype=np.float32)
+    h = v.astype(np.float16)
+    h = np.where(h.astype(np.float32) < v, np.nextafter(h, np.float16(np.inf)), h)
+    return h.astype(np.float64)
+
+
+def analyse_cthr(terms, frags, rinfo, accept, B, tau, T_tau, bnd):
+    """One probe run of MfmaSpec::cthr (layout 3): terms [..., 0:3] and 4 are
+    U, -V, X, Y with TT = -Tl'' as their accumulator, terms[..., 3] is TT.
+    Checks TT against its construction (the wave's factors padded by 2^-8 and
+    rounded up to f16, times the record's -tau, -CH, -CL) and against the
+    5-product threshold Tl' it must exceed; the shifted terms' accumulation
+    error against the exact sum of their f16 products plus TT; and that every
+    reference-accepted pair passes (all four shifted terms negative: the sign
+    bit of U & V & X & Y)."""
+    n_tris = accept.shape[1]
+    live = rinfo[:, 0] == 1.0
+    hw = terms[live][:, :n_tris, :].astype(np.float64)
+    B = B.copy()
+    B[:, :3, 16:18] = 0.0
+    fw = np.abs(frags.astype(np.float32)).reshape(-1, 64, 48)
+    zlo = np.repeat(fw[:, :, 16].max(1), 64)[live].astype(np.float64)
+    zhi = np.repeat(fw[:, :, 17].max(1), 64)[live].astype(np.float64)
+    ch, cl = bnd[0][:n_tris].astype(np.float64), bnd[1][:n_tris].astype(np.float64)
+    Tw = rinfo[live, 2]
+    pad = np.float32(1.00390625)
+    tt = T_tau[:n_tris].astype(np.float64)
+    Tl2 = (tt[None, :] * f16_up(Tw * pad)[:, None] + ch[None, :] * f16_up(zlo.astype(np.float32) * pad)[:, None]
+           + cl[None, :] * f16_up(zhi.astype(np.float32) * pad)[:, None])
+    Tl1 = (T_tau[None, :n_tris].astype(np.float32) * Tw[:, None].astype(np.float32)).astype(np.float64) + \
+        (ch[None, :] * zlo[:, None] + cl[None, :] * zhi[:, None]) * (1 + 2.0 ** -10)
+    TT = hw[..., 3]
+    tt_err = np.abs(TT + Tl2) / Tl2
+    fr = frags[live].astype(np.float64)
+    A_main = fr[:, :32]
+    A_y = np.concatenate([np.zeros((len(fr), 16)), fr[:, 32:48]], 1)
+    exact = np.empty(hw.shape[:2] + (4,))
+    sabs = np.empty_like(exact)
+    for j, q in enumerate((0, 1, 2)):
+        exact[..., j] = A_main @ B[:, q, :].T
+        sabs[..., j] = np.abs(A_main) @ np.abs(B[:, q, :]).T
+    exact[..., 3] = A_y @ B[:, 3, :].T
+    sabs[..., 3] = np.abs(A_y) @ np.abs(B[:, 3, :]).T
+    sh = hw[..., [0, 1, 2, 4]]
+    acc_err = np.abs(sh - (exact + TT[..., None]))
+    ulp = 2.0 ** -24 * (sabs + np.abs(TT)[..., None])
+    acc_ratio = acc_err / np.where(ulp > 0, ulp, 1.0)
+    sign = sh.astype(np.float32).view(np.int32) < 0
+    passes = sign.all(-1)
+    acc = accept[live]
+    violations = np.argwhere(acc & ~passes)
+    out = {
+        "rays_in_range": int(live.sum()), "pairs": int(acc.size), "accepted_pairs": int(acc.sum()),
+        "filter_pass_frac": float(passes.mean()),
+        "tt_rel_err_max": float(tt_err.max()),
+        "tt_over_Tl_min": float((-TT / Tl1).min()),
+        "acc_err_max_in_2^-24_sum_abs": float(acc_ratio.max()),
+        "acc_err_bound_assumed": 31.0,
+        "violations": int(len(violations)),
+    }
+    return out, violations
+
+
 def _unit(v):
     return v / np.linalg.norm(v, axis=-1, keepdims=True)
 

@@ -156,14 +156,50 @@ def test_matrix_filter_k5_conservative(checker, seed):
     assert passes_y <= passes <= passes_y * 1.03 and p_near <= p_near_y * 1.03
 
 
+def _run_cthr(exe, n, seed):
+    """(violations, passes, passes at ordinary scales) of the threshold-in-
+    the-accumulator form (MfmaSpec::cthr) and (violations of the 5-product
+    form, passes and passes at ordinary scales of that form without its -tn
+    term, the one cthr restates), on the same draws."""
+    out = subprocess.run([exe, str(n), str(seed)], check=True, capture_output=True, text=True).stdout
+    v = tuple(map(int, out.split()))
+    return v[19:22], (v[16], v[22], v[23])
+
+
+@pytest.mark.parametrize("seed", [10, 11])
+def test_matrix_filter_cthr_conservative(checker, seed):
+    """MfmaSpec::cthr: the threshold enters every term through the
+    accumulator (TT = -(tau Tw + CH ML + CL MH), its factors padded and
+    rounded up to f16) and a pair passes iff all four shifted terms are
+    negative.  No accepted pair is skipped, and it passes no more than a
+    percent beyond the 5-product form it restates (the pad)."""
+    (bad, passes, p_near), (bad5, passes5, p_near5) = _run_cthr(checker, 2_000_000, seed)
+    assert bad == 0 and bad5 == 0
+    assert passes5 <= passes <= passes5 * 1.01 and p_near <= p_near5 * 1.01
+
+
+def test_harness_detects_cthr_without_its_threshold(tmp_path):
+    """With TT = 0 (no threshold in the accumulator) the sign test skips
+    accepted pairs: the harness sees it."""
+    src = open(SRC).read()
+    old = "        TT = -s3 * (1.0 - 0x1p-23);"
+    assert old in src
+    p = tmp_path / "mut.c"
+    p.write_text(src.replace(old, "        TT = 0.0 * s3;"))
+    exe = str(tmp_path / "mut")
+    subprocess.run(["gcc", "-O2", "-std=c11", "-ffp-contract=off", "-o", exe, str(p), "-lm"], check=True)
+    (bad, _, _), _ = _run_cthr(exe, 1_000_000, 1)
+    assert bad > 0
+
+
 def test_harness_detects_k5_without_its_bound(tmp_path):
     """Leaving out the m.z slots without raising the threshold skips accepted
     pairs: the bound is necessary, and the harness sees its absence."""
     src = open(SRC).read()
-    old = "    if (k5) {\n        float ch"
+    old = "    } else if (k5) {\n        float ch"
     assert old in src
     p = tmp_path / "mut.c"
-    p.write_text(src.replace(old, "    if (0) {\n        float ch"))
+    p.write_text(src.replace(old, "    } else if (0) {\n        float ch"))
     exe = str(tmp_path / "mut")
     subprocess.run(["gcc", "-O2", "-std=c11", "-ffp-contract=off", "-o", exe, str(p), "-lm"], check=True)
     (bad, _, _), _ = _run_k5(exe, 1_000_000, 1)

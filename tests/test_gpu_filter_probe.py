@@ -97,6 +97,36 @@ def test_filter_terms_on_hardware(rt2mod, torch_cuda, kind, layout):
         assert (pad_bits > Tl.view(np.int32)).all()
 
 
+@pytest.mark.parametrize("kind", KINDS)
+def test_filter_cthr_on_hardware(rt2mod, torch_cuda, kind):
+    """MfmaSpec::cthr on the hardware: the threshold product TT is -Tl'' as
+    constructed (within the f32 rounding of three exact products) and at
+    least the 5-product threshold Tl'; the shifted terms are their f16
+    products' exact sum plus TT within the assumed accumulation bound; every
+    pair the reference accepts has all four shifted terms negative."""
+    rng = np.random.default_rng(200 + KINDS.index(kind))
+    V, rays = fpl.scene_and_rays(kind, rng)
+    scene = rt2mod.Scene(triangles=_tri_array(rt2mod, V), materials=_materials(rt2mod))
+    B = fpl.records_k16(scene.export(3, np.uint16), len(V))
+    T_tau = scene.export(4, np.float32)
+    dev = scene.export(5, np.float32).reshape(-1, 2)[:len(V)]
+    bnd = fpl.k5_bounds(B)
+    np.testing.assert_array_equal(dev[:, 0], bnd[0])
+    # the -tn record's threshold slots: -tau, -CH, -CL
+    np.testing.assert_array_equal(B[:, 3, 29], -T_tau[:len(V)].astype(np.float64))
+    np.testing.assert_array_equal(B[:, 3, 30], -bnd[0].astype(np.float64))
+    np.testing.assert_array_equal(B[:, 3, 31], -bnd[1].astype(np.float64))
+    terms, frags, rinfo, accept = scene.mfma_probe(3, rays)
+    st, viol = fpl.analyse_cthr(terms, frags, rinfo, accept, B, None, T_tau, bnd)
+    _results[f"{kind}/cthr"] = st
+    assert st["rays_in_range"] >= len(rays) // 2
+    assert st["accepted_pairs"] > 0
+    assert st["tt_rel_err_max"] <= 2.0 ** -22, st
+    assert st["tt_over_Tl_min"] > 1.0, st
+    assert st["acc_err_max_in_2^-24_sum_abs"] <= st["acc_err_bound_assumed"], st
+    assert st["violations"] == 0, f"reference-accepted pairs rejected by the cthr filter: {viol[:10]}"
+
+
 def test_write_probe_summary():
     out = os.environ.get("RT2_PROBE_OUT")
     if not out or not _results:
@@ -151,7 +181,7 @@ def near_threshold_scene(rt2mod):
     return sd
 
 
-@pytest.mark.parametrize("variant", [150, 152, 200, 206, 227, 228, 231, 233, 212, 213, 237, 238, 243, 245, 247, 248, 249, 250, 252])
+@pytest.mark.parametrize("variant", [150, 152, 200, 206, 227, 228, 231, 233, 212, 213, 214, 215, 216, 217, 260, 261, 237, 238, 243, 245, 247, 248, 249, 250, 252])
 def test_near_threshold_scene_bit_exact(rt2mod, oraclemod, torch_cuda, variant):
     if not rt2mod.has_variant(variant):
         pytest.skip(f"variant {variant} not in this build")
