@@ -75,7 +75,8 @@ struct MfmaSpec {
     bool wg_pool = false;   // render_mfma_pool (rt2_k5_pool.h): the workgroup's rays packed into 32-ray blocks
     bool wg_split = false;  // ... and with <= 2 blocks, each block's sweep split over the waves by triangle range
     int tile_bufs = 2;      // render_mfma_k5t: record tile buffers (3: tile t+2 in flight while t is swept)
-    bool ylds = false;      // cthr: each block's main and Y fragments are read from LDS right before its products
+    int ylds = 0;           // cthr: each block's Y fragment (1), or its main and Y fragments (2), read from LDS right
+                            // before its products
     bool cthr = false;      // k5 no_tn: the threshold rides in the products' accumulator operand (one matrix
                             // product per group, mfma_thr_frag), and the reduction is a sign-bit AND / OR
                             // (2 v_bitop3_b32 per pair instead of 2.5 min / max)
@@ -726,7 +727,7 @@ __device__ __forceinline__ unsigned long long k5_cthr_group(ThrBits tb, const h8
 #pragma unroll
     for (int R = 0; R < 2; R++) {
         if (R == 1 && !upper) break;
-        const h8 aR = S.ylds ? *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][8 * hl]) : a0[R];
+        const h8 aR = S.ylds == 2 ? *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][8 * hl]) : a0[R];
         const f16v U = __builtin_amdgcn_mfma_f32_32x32x16_f16(aR, b0, TT, 0, 0, 0);
         const f16v V = __builtin_amdgcn_mfma_f32_32x32x16_f16(aR, b2, TT, 0, 0, 0);
         const f16v X = __builtin_amdgcn_mfma_f32_32x32x16_f16(aR, b4, TT, 0, 0, 0);
@@ -805,7 +806,7 @@ __device__ __forceinline__ bool sweep_k16(const RenderParams& p, SH& sh, const f
 #pragma unroll
         for (int R = 0; R < 2; R++) y1[R] = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][YO + 8 * hl]);
     };
-    if constexpr (!S.afrag_lds && !S.ylds) read_a();
+    if constexpr (!S.afrag_lds && S.ylds < 2) read_a();
     if constexpr (!S.ylds) read_y();
     [[maybe_unused]] ThrBits thr = {};
     if constexpr (S.cthr) thr = mfma_thr_bits(sc.Tw, zlo, zhi);

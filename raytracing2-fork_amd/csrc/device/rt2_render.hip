@@ -669,18 +669,22 @@ const Variant kVariants[] = {
     // default brute-force kernel (DESIGN.md "The 5-product form"): the k16 sweep with U, -V, X from the first K-half,
     // the left-out m.z slots bounded in the threshold; 3 waves per SIMD, and 4 for launches with < 1.5 items per lane
     RT2_VARIANT(227, K_MFMA, render_mfma<kMfmaK5>, 256, "mfma/256/k5/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"),
-    // scenes of <= 8,192 triangles (records L2-resident): the same without the -tn term (4 products per block),
-    // 4 waves (packed path state; 243), or 3 when the packed fields do not hold the image / rays / bounces (231)
-    RT2_VARIANT(231, K_MFMA, render_mfma<kMfmaK5NoTn>, 256, "mfma/256/k5/notn/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"),
-    RT2_VARIANT(243, K_MFMA, render_mfma<kMfmaK5NoTnW4C4>, 256, "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
-    // LDS record tiles shared by the workgroup (rt2_k5_tiles.h; DESIGN.md "LDS record tiles"): 213 the default
-    // above 8,192 triangles (10-group tiles, path state in registers), 252 the first form (4-group tiles, path
-    // state parked in LDS)
-    RT2_VARIANT(213, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(10, true, 0); x.rows80 = true; x.lane_lds = 0; return x; }()>, 768, "mfmat5/768/k5/notn/tile10/coop0/w3/cmp/rows80/regs"),
-    RT2_VARIANT(252, K_MFMA, render_mfma_k5t<k5_tiles_spec(4, true, 0)>, 768, "mfmat5/768/k5/notn/tile4/coop0/w3/llds2/cmp"),
+    // scenes of <= 8,192 triangles (records L2-resident): the same without the -tn term (4 products per block) and
+    // with the threshold in the products' accumulator (MfmaSpec::cthr, DESIGN.md "The threshold in the
+    // accumulator"), 4 waves (packed path state, Y fragments read per block: 263), or 3 when the packed fields do not
+    // hold the image / rays / bounces (262)
+    RT2_VARIANT(263, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4C4; x.cthr = true; x.ylds = 1; return x; }()>, 256, "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp/cthr/yl1"),
+    RT2_VARIANT(262, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTn; x.cthr = true; return x; }()>, 256, "mfma/256/k5/notn/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp/cthr"),
+    // LDS record tiles shared by the workgroup (rt2_k5_tiles.h; DESIGN.md "LDS record tiles"), the default above
+    // 8,192 triangles: 10-group tiles, path state in registers, the threshold in the accumulator
+    RT2_VARIANT(217, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(10, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile10/coop0/w3/cmp/rows80/regs/cthr"),
 #ifdef RT2_EXPERIMENTS
     // earlier product kernels (round 2's 16x16x32 form; round 3's k16 sweep and 5-product choices; round 4's
-    // first tile form with -tn), kept for A/B
+    // first tile forms and the small-scene kernels before the threshold moved into the accumulator), kept for A/B
+    RT2_VARIANT(231, K_MFMA, render_mfma<kMfmaK5NoTn>, 256, "mfma/256/k5/notn/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"),
+    RT2_VARIANT(243, K_MFMA, render_mfma<kMfmaK5NoTnW4C4>, 256, "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
+    RT2_VARIANT(213, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(10, true, 0); x.rows80 = true; x.lane_lds = 0; return x; }()>, 768, "mfmat5/768/k5/notn/tile10/coop0/w3/cmp/rows80/regs"),
+    RT2_VARIANT(252, K_MFMA, render_mfma_k5t<k5_tiles_spec(4, true, 0)>, 768, "mfmat5/768/k5/notn/tile4/coop0/w3/llds2/cmp"),
     RT2_VARIANT(228, K_MFMA, render_mfma<kMfmaK5W4>, 256, "mfma/256/k5/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
     RT2_VARIANT(233, K_MFMA, render_mfma<kMfmaK5NoTnW4>, 256, "mfma/256/k5/notn/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
     RT2_VARIANT(250, K_MFMA, render_mfma_k5t<k5_tiles_spec(4, false, 0)>, 768, "mfmat5/768/k5/tile4/coop0/w3/llds2/cmp"),
@@ -697,9 +701,8 @@ const Variant kVariants[] = {
     RT2_VARIANT(238, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(6, true, 0); x.rows80 = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile6/coop0/w3/llds2/cmp/rows80"),
     RT2_VARIANT(214, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(10, true, 0); x.rows80 = true; x.lane_lds = 0; x.prefetch = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile10/coop0/w3/cmp/rows80/regs/pf"),
     RT2_VARIANT(215, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(10, true, 8); x.rows80 = true; x.lane_lds = 0; return x; }()>, 768, "mfmat5/768/k5/notn/tile10/coop8/w3/cmp/rows80/regs"),
-    RT2_VARIANT(217, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(10, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile10/coop0/w3/cmp/rows80/regs/cthr"),
     RT2_VARIANT(260, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4C4; x.cthr = true; return x; }()>, 256, "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp/cthr"),
-    RT2_VARIANT(261, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4C4; x.cthr = true; x.ylds = true; return x; }()>, 256, "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp/cthr/ylds"),
+    RT2_VARIANT(261, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4C4; x.cthr = true; x.ylds = 2; return x; }()>, 256, "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp/cthr/ylds"),
     RT2_VARIANT(216, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(11, true, 0); x.rows80 = true; x.lane_lds = 0; return x; }()>, 768, "mfmat5/768/k5/notn/tile11/coop0/w3/cmp/rows80/regs"),
     RT2_VARIANT(212, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(8, true, 0); x.rows80 = true; x.lane_lds = 0; return x; }()>, 768, "mfmat5/768/k5/notn/tile8/coop0/w3/cmp/rows80/regs"),
     RT2_VARIANT(258, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(4, true, 0); x.prefetch = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile4/coop0/w3/llds2/cmp/pf"),
@@ -859,13 +862,14 @@ constexpr int kDefaultBvh = 109;
 constexpr int kLargeScene = 86;  // tiled/512/max3f4: LDS tiles above kSmemMaxTris triangles
 constexpr int kSlab = 92;        // assist12/max3f8/w6: fewer than 4 items per lane (multi-GPU slabs)
 constexpr int kMfmaSlabMaxTris = 8192;
-constexpr int kMfmaSmall = 243;    // <= kMfmaSlabMaxTris triangles: k5 without -tn, 4 waves (packed path state),
-                                   // cooperative drain at <= 4 live rays (config B 187.9 vs 192.9 ms for 233's 8)
-constexpr int kMfmaSmallW3 = 231;  // ... 3 waves, when the packed fields cannot hold the launch
-constexpr int kMfmaTiles = 213;    // larger scenes: the 5-product form without -tn with workgroup-shared LDS record
+constexpr int kMfmaSmall = 263;    // <= kMfmaSlabMaxTris triangles: k5 without -tn, 4 waves (packed path state),
+                                   // cooperative drain at <= 4 live rays (config B 187.9 vs 192.9 ms for 233's 8), the
+                                   // threshold in the accumulator (DESIGN.md "The threshold in the accumulator")
+constexpr int kMfmaSmallW3 = 262;  // ... 3 waves, when the packed fields cannot hold the launch
+constexpr int kMfmaTiles = 217;    // larger scenes: the 5-product form without -tn with workgroup-shared LDS record
                                    // tiles of 10 groups, the path state in registers (rt2_k5_tiles.h; DESIGN.md "LDS
-                                   // record tiles"): config C 25.94 vs 26.66 s for 252's 4-group tiles and 32.5 s for
-                                   // round 3's 227
+                                   // record tiles": config C 25.94 vs 26.66 s for 252's 4-group tiles and 32.5 s for
+                                   // round 3's 227), the threshold in the accumulator (C sample 1.07 vs 1.24 s for 213)
 constexpr int kMfma = 227;  // mfma/.../k5/...: the matrix-core filter on v_mfma_f32_32x32x16_f16, 5 products per
                             // 32-ray block (DESIGN.md "The 5-product form"), registers only; larger scenes whose
                             // packed path state cannot hold the launch

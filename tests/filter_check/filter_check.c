@@ -240,7 +240,8 @@ static double f16_up(float v) {
 /* k5 = 2 (MfmaSpec::cthr): the same 4-term form with the threshold in the
  * accumulator: TT = -(tau Tw'' + CH ML'' + CL MH'') from the -tn record's
  * slots 29..31 (-tau, -CH, -CL) times mfma_thr_frag's f16 factors (padded by
- * 2^-8, rounded up), its 3-term f32 sum moved toward zero by 2u; each term is
+ * 2^-8, rounded up), its 3-term sum moved toward zero by 2^-12 (the matrix
+ * core's measured worst is 2^-18.6, tests/test_gpu_filter_probe.py); each term is
  * its products plus TT, moved by 31 u (sum |p| + |TT|) toward rejection, and
  * passes iff negative (the sign-bit AND). */
 static int pass_mfma(f3 o, f3 d, double slot[MQ][32], double tau, float As, float Ow, float Mw, float bestK,
@@ -276,7 +277,7 @@ static int pass_mfma(f3 o, f3 d, double slot[MQ][32], double tau, float As, floa
         const float pad = 1.00390625f;
         const double s3 = (double)(float)tau * f16_up(Tw * pad) + (double)ch * f16_up((float)fabs(ray[16]) * pad) +
                           (double)cl * f16_up((float)fabs(ray[17]) * pad);
-        TT = -s3 * (1.0 - 0x1p-23);
+        TT = -s3 * (1.0 - 0x1p-12);
     } else if (k5) {
         float ch = 0.0f, cl = 0.0f;
         for (int q = 0; q < 3; q++) ch = fmaxf(ch, (float)fabs(slot[q][16])), cl = fmaxf(cl, (float)fabs(slot[q][17]));

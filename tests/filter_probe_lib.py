@@ -205,6 +205,13 @@ def analyse_cthr(terms, frags, rinfo, accept, B, tau, T_tau, bnd):
         (ch[None, :] * zlo[:, None] + cl[None, :] * zhi[:, None]) * (1 + 2.0 ** -10)
     TT = hw[..., 3]
     tt_err = np.abs(TT + Tl2) / Tl2
+    w = np.unravel_index(np.argmax(tt_err), tt_err.shape)
+    r_, t_ = int(w[0]), int(w[1])
+    worst = {"TT": float(TT[w]), "Tl2": float(Tl2[w]), "Tl1": float(Tl1[w]),
+             "tau": float(tt[t_]), "Tw": float(Tw[r_]), "zlo": float(zlo[r_]), "zhi": float(zhi[r_]),
+             "ch": float(ch[t_]), "cl": float(cl[t_]),
+             "Tw16": float(f16_up(Tw[r_] * pad)), "zlo16": float(f16_up(np.float32(zlo[r_]) * pad)),
+             "zhi16": float(f16_up(np.float32(zhi[r_]) * pad))}
     fr = frags[live].astype(np.float64)
     A_main = fr[:, :32]
     A_y = np.concatenate([np.zeros((len(fr), 16)), fr[:, 32:48]], 1)
@@ -227,6 +234,7 @@ def analyse_cthr(terms, frags, rinfo, accept, B, tau, T_tau, bnd):
         "rays_in_range": int(live.sum()), "pairs": int(acc.size), "accepted_pairs": int(acc.sum()),
         "filter_pass_frac": float(passes.mean()),
         "tt_rel_err_max": float(tt_err.max()),
+        "tt_worst": worst,
         "tt_over_Tl_min": float((-TT / Tl1).min()),
         "acc_err_max_in_2^-24_sum_abs": float(acc_ratio.max()),
         "acc_err_bound_assumed": 31.0,

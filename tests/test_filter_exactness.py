@@ -182,7 +182,7 @@ def test_harness_detects_cthr_without_its_threshold(tmp_path):
     """With TT = 0 (no threshold in the accumulator) the sign test skips
     accepted pairs: the harness sees it."""
     src = open(SRC).read()
-    old = "        TT = -s3 * (1.0 - 0x1p-23);"
+    old = "        TT = -s3 * (1.0 - 0x1p-12);"
     assert old in src
     p = tmp_path / "mut.c"
     p.write_text(src.replace(old, "        TT = 0.0 * s3;"))

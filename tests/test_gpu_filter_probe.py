@@ -100,8 +100,8 @@ def test_filter_terms_on_hardware(rt2mod, torch_cuda, kind, layout):
 @pytest.mark.parametrize("kind", KINDS)
 def test_filter_cthr_on_hardware(rt2mod, torch_cuda, kind):
     """MfmaSpec::cthr on the hardware: the threshold product TT is -Tl'' as
-    constructed (within the f32 rounding of three exact products) and at
-    least the 5-product threshold Tl'; the shifted terms are their f16
+    constructed (within 2^-12 of the exact sum of its three exact products)
+    and beyond the 5-product threshold Tl'; the shifted terms are their f16
     products' exact sum plus TT within the assumed accumulation bound; every
     pair the reference accepts has all four shifted terms negative."""
     rng = np.random.default_rng(200 + KINDS.index(kind))
@@ -119,12 +119,16 @@ def test_filter_cthr_on_hardware(rt2mod, torch_cuda, kind):
     terms, frags, rinfo, accept = scene.mfma_probe(3, rays)
     st, viol = fpl.analyse_cthr(terms, frags, rinfo, accept, B, None, T_tau, bnd)
     _results[f"{kind}/cthr"] = st
+    print(json.dumps(st, indent=1))
     assert st["rays_in_range"] >= len(rays) // 2
     assert st["accepted_pairs"] > 0
-    assert st["tt_rel_err_max"] <= 2.0 ** -22, st
+    assert st["violations"] == 0, f"reference-accepted pairs rejected by the cthr filter: {viol[:10]}"
     assert st["tt_over_Tl_min"] > 1.0, st
     assert st["acc_err_max_in_2^-24_sum_abs"] <= st["acc_err_bound_assumed"], st
-    assert st["violations"] == 0, f"reference-accepted pairs rejected by the cthr filter: {viol[:10]}"
+    # the matrix core's sum of the three threshold products: up to 2^-18.6 below
+    # the exact sum on this data (measured; smaller products lose low bits in
+    # the alignment), which the 2^-8 pad covers many times over
+    assert st["tt_rel_err_max"] <= 2.0 ** -12, st
 
 
 def test_write_probe_summary():
@@ -136,10 +140,14 @@ def test_write_probe_summary():
         "T": "2^-12 (Omax + A + 1) sigma tau (MfmaSpec::tshift = 12)",
         "worst": {
             "acc_err_max_in_2^-24_sum_abs": max(v["acc_err_max_in_2^-24_sum_abs"] for v in _results.values()),
-            "total_err_max_over_T": max(v["total_err_max_over_T"] for v in _results.values()),
+            "total_err_max_over_T": max(v.get("total_err_max_over_T", 0.0) for v in _results.values()),
             "violations": sum(v["violations"] for v in _results.values()),
             "accepted_pairs": sum(v["accepted_pairs"] for v in _results.values()),
-            "accepted_within_T_of_a_boundary": sum(v["accepted_within_T_of_a_boundary"] for v in _results.values()),
+            "accepted_within_T_of_a_boundary": sum(v.get("accepted_within_T_of_a_boundary", 0) for v in _results.values()),
+            "cthr_tt_rel_err_max": max((v["tt_rel_err_max"] for v in _results.values() if "tt_rel_err_max" in v),
+                                       default=None),
+            "cthr_tt_over_Tl_min": min((v["tt_over_Tl_min"] for v in _results.values() if "tt_over_Tl_min" in v),
+                                       default=None),
         },
         "cases": _results,
     }
@@ -181,7 +189,7 @@ def near_threshold_scene(rt2mod):
     return sd
 
 
-@pytest.mark.parametrize("variant", [150, 152, 200, 206, 227, 228, 231, 233, 212, 213, 214, 215, 216, 217, 260, 261, 237, 238, 243, 245, 247, 248, 249, 250, 252])
+@pytest.mark.parametrize("variant", [150, 152, 200, 206, 227, 228, 231, 233, 212, 213, 214, 215, 216, 217, 260, 261, 262, 263, 237, 238, 243, 245, 247, 248, 249, 250, 252])
 def test_near_threshold_scene_bit_exact(rt2mod, oraclemod, torch_cuda, variant):
     if not rt2mod.has_variant(variant):
         pytest.skip(f"variant {variant} not in this build")

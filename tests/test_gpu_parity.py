@@ -100,9 +100,9 @@ def _last_variant(rt2mod, scene):
     return rt2mod.lib().rt2_variant_name(lv.value).decode()
 
 
-AUTO_TILES = "mfmat5/768/k5/notn/tile10/coop0/w3/cmp/rows80/regs"  # variant 213: > 8,192 triangles, LDS record tiles
-AUTO_SMALL = "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp"  # 243: <= 8,192 triangles
-AUTO_SMALL_W3 = "mfma/256/k5/notn/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"  # 231: packed fields too small
+AUTO_TILES = "mfmat5/768/k5/notn/tile10/coop0/w3/cmp/rows80/regs/cthr"  # variant 217: > 8,192 triangles, LDS record tiles
+AUTO_SMALL = "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp/cthr/yl1"  # 263: <= 8,192 triangles
+AUTO_SMALL_W3 = "mfma/256/k5/notn/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp/cthr"  # 262: packed fields too small
 
 
 def test_auto_variant_large_scene(rt2mod, oraclemod, config_scene, torch_cuda):
@@ -332,11 +332,11 @@ def test_frame_split_identical(rt2mod, oraclemod, config_scene, torch_cuda, trav
 
 
 # brute-force kernel variants that change the schedule, not the arithmetic:
-# the product variants (0 = automatic, 86, 92, 227/231/243 = the matrix filter, 213/252 = its LDS-tiled form,
+# the product variants (0 = automatic, 86, 92, 227/262/263 = the matrix filter, 217 = its LDS-tiled form,
 # 136 = the scalar path forced) and, in an experiment build, the A/B
 # variants (masked/plk filters, resident LDS, cooperative and team tail modes,
 # split waves, the round-1 slab kernels, occupancy hints)
-BRUTE_VARIANTS = [0, 86, 92, 213, 227, 231, 243, 252, 136] + ([150, 152, 200, 206, 228, 233, 250, 137, 138, 139, 140, 143, 144, 145, 146] if EXPERIMENTS else []) + ([22, 24, 28, 52, 64, 65, 66, 67, 68, 70, 71, 72, 73, 74, 76, 79, 80, 84, 85, 87, 89, 95, 97, 101, 104, 106,
+BRUTE_VARIANTS = [0, 86, 92, 217, 227, 262, 263, 136] + ([213, 231, 243, 252, 260, 261, 150, 152, 200, 206, 228, 233, 250, 137, 138, 139, 140, 143, 144, 145, 146] if EXPERIMENTS else []) + ([22, 24, 28, 52, 64, 65, 66, 67, 68, 70, 71, 72, 73, 74, 76, 79, 80, 84, 85, 87, 89, 95, 97, 101, 104, 106,
                                  90] if EXPERIMENTS else [])
 
 
