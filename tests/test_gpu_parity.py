@@ -92,6 +92,35 @@ def test_config_B_full_size_rows_exact(rt2mod, oraclemod, config_scene, torch_cu
     assert np.sqrt((d ** 2).mean()) < RMSE_TOL
 
 
+@pytest.mark.parametrize("cfg,W,H", [("B", 1920, 1080), ("C", 480, 270), ("E", 240, 135)],
+                         ids=["B-full", "C-480x270", "E-240x135"])
+def test_full_frame_every_pixel(rt2mod, oraclemod, config_scene, torch_cuda, cfg, W, H):
+    """Every pixel of a whole frame, by a traversal cross-check: the GPU BVH
+    image equals the oracle's BVH image bit for bit at every pixel; the GPU
+    brute-force image (the automatic matrix kernel) equals it too except where
+    the two traversals may legitimately differ (exact distance ties), and at
+    each such pixel, plus 96 random ones, it equals the oracle's brute force.
+    (The oracle's brute force over a whole config C frame would take hours;
+    its BVH mode takes seconds.)"""
+    sd, spec = config_scene(cfg)
+    u = rt2mod.offline_uniforms(W, H, spec.bounces, spec.rays, sd.num_triangles)
+    scene = rt2mod.Scene(sd, 0)
+    img = scene.render_host(u, 0, 1)
+    assert _last_variant(rt2mod, scene) == (AUTO_SMALL if cfg == "B" else AUTO_TILES)
+    st = scene.stats(reset=True)
+    assert st.samples == W * H * spec.rays
+    scene.set_traversal("bvh")
+    img_bvh = scene.render_host(u, 0, 1)
+    ref_bvh, _, _ = oracle_mean(oraclemod, sd, u, np.arange(H), 0, 1, "bvh")
+    assert_exact(img_bvh, ref_bvh, f"config {cfg} GPU BVH, whole frame")
+    diff = np.argwhere((img[..., :3] != ref_bvh).any(-1))
+    assert len(diff) <= max(W * H // 10000, 8), f"{len(diff)} pixels where brute force and BVH differ"
+    rng = np.random.default_rng(7)
+    pick = np.concatenate([diff, np.stack([rng.integers(0, H, 96), rng.integers(0, W, 96)], 1)])
+    acc, _, _, _ = oraclemod.render_pixels(sd.triangles(), sd.materials(), u, pick[:, 1], pick[:, 0], 0, 1, "brute")
+    assert_exact(img[pick[:, 0], pick[:, 1]], acc[:, :3], f"config {cfg} brute force at {len(diff)} + 96 pixels")
+
+
 def _last_variant(rt2mod, scene):
     import ctypes as C
     c = (C.c_ulonglong * 8)()
