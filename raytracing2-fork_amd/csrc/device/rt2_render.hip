@@ -40,6 +40,7 @@ using namespace rt2d;
 #include "rt2_mfma.h"
 #include "rt2_k5_tiles.h"
 #include "rt2_k5_pool.h"
+#include "rt2_k5_dtiles.h"
 #include "rt2_assist.h"
 #include "rt2_bvh.h"
 #include "rt2_misc_kernels.h"
@@ -703,6 +704,8 @@ const Variant kVariants[] = {
     RT2_VARIANT(215, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(10, true, 8); x.rows80 = true; x.lane_lds = 0; return x; }()>, 768, "mfmat5/768/k5/notn/tile10/coop8/w3/cmp/rows80/regs"),
     RT2_VARIANT(260, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4C4; x.cthr = true; return x; }()>, 256, "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp/cthr"),
     RT2_VARIANT(261, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4C4; x.cthr = true; x.ylds = 2; return x; }()>, 256, "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp/cthr/ylds"),
+    RT2_VARIANT(269, K_MFMA, render_mfma_k5d<[] { MfmaSpec x = k5_tiles_spec(10, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; return x; }()>, 768, "mfmat5d/768/k5/notn/tile10/coop0/w3/cmp/rows80/regs/cthr/dec"),
+    RT2_VARIANT(270, K_MFMA, render_mfma_k5d<[] { MfmaSpec x = k5_tiles_spec(6, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; return x; }()>, 768, "mfmat5d/768/k5/notn/tile6/coop0/w3/cmp/rows80/regs/cthr/dec"),
     RT2_VARIANT(216, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(11, true, 0); x.rows80 = true; x.lane_lds = 0; return x; }()>, 768, "mfmat5/768/k5/notn/tile11/coop0/w3/cmp/rows80/regs"),
     RT2_VARIANT(212, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(8, true, 0); x.rows80 = true; x.lane_lds = 0; return x; }()>, 768, "mfmat5/768/k5/notn/tile8/coop0/w3/cmp/rows80/regs"),
     RT2_VARIANT(258, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(4, true, 0); x.prefetch = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile4/coop0/w3/llds2/cmp/pf"),
