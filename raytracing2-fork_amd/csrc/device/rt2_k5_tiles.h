@@ -20,9 +20,13 @@
 // the result is the sequential strict `dst < best` scan's bit for bit.
 //
 // Register budget: the k16 tiled attempt (render_mfma_tiled) kept the path
-// state in VGPRs across the tile loop and spilled 45 of them; this kernel
-// parks it in LDS (the packed 15-word stash of the 4-wave build) in every
-// wave, sweeping or not, so that no path state is live across the loop.
+// state in VGPRs across the tile loop and spilled 45 of them.  The first form
+// here (MfmaSpec::lane_lds = 2, variant 252) parks it in LDS (the packed
+// 15-word stash of the 4-wave build); with round 4's register changes and
+// 80-B fragment rows it fits in registers (lane_lds = 0, rows80: variants
+// 213 and 217, 10-group tiles), and with MfmaSpec::cthr the threshold rides
+// in the products' accumulator (k5_cthr_group), so the tiles carry no bounds
+// or scales.
 #pragma once
 
 namespace {
