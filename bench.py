@@ -61,14 +61,14 @@ BVH_RECORD_BYTES = 64      # BVH: one child-pair record per interior visit (both
 BVH_TRI_BYTES = 48         # BVH: one pre-transformed triangle record per leaf test
 L2_PEAK_GBS = 34500.0      # MI355X_MICROARCH.md §L2: ≈34.5 TB/s aggregate
 MFMA_F16_PEAK_TFLOPS = 2500.0  # MI355X dense F16/BF16 matrix peak (MI355X_MICROARCH.md; no sparsity)
-MFMA_F16_SUSTAINED_TFLOPS = 1240.0  # measured: 16 v_mfma_f32_32x32x16_f16 per 417-450 ns per SIMD at 2-4 waves (1.19-1.29 PF; overlap probe)
+MAX_CLOCK_GHZ = 2.4        # MI355X_MICROARCH.md chip-level parameters: the clock the dense peaks are quoted at
 MFMA_FLOP_PER_PAIR = 320   # render_mfma 16x16x32 form: 5 quantities x 32 k-slots x 2 per (ray, triangle) pair
 MFMA_K16_FLOP_PER_PAIR = 256  # the k16 sweep: 8 v_mfma_f32_32x32x16_f16 (32x32x16x2 FLOP each) per 1,024 pairs
 MFMA_K5_FLOP_PER_PAIR = 160   # its 5-product form (MfmaSpec::k5): 5 v_mfma_f32_32x32x16_f16 per 1,024 pairs
 MFMA_K5_NOTN_FLOP_PER_PAIR = 128  # ... without the -tn term (small scenes): 4 per 1,024 pairs
 SCALAR_VARIANT = 136       # render_smem forced (rt2_render.hip): the no-MFMA scalar-path kernel
 TARGET_RATIO = 10.0        # north star: >= 10x the CPU reference at config C on 1 GPU
-KERNEL_FILES = {"mfmat5": "render_mfma_k5t", "mfma": "render_mfma", "massist": "render_assist", "smem": "render_smem", "split": "render_split", "tiled": "render_tiled", "assist": "render_assist",
+KERNEL_FILES = {"mfmat5": "render_mfma_k5t", "mfmar": "render_mfma_k5r", "mfma": "render_mfma", "massist": "render_assist", "smem": "render_smem", "split": "render_split", "tiled": "render_tiled", "assist": "render_assist",
                 "resident": "render_resident", "bvh4": "render_bvh4", "bvh3": "render_bvh3", "bvh2": "render_bvh2",
                 "bvh": "render_bvh"}
 
@@ -159,6 +159,7 @@ KERNEL_SOURCES = ["raytracing2-fork_amd/csrc/device/rt2_math.h", "raytracing2-fo
 KERNEL_SOURCES_BY_TRAVERSAL = {"brute": ["raytracing2-fork_amd/csrc/device/rt2_brute.h",  # the brute-force kernels
                                          "raytracing2-fork_amd/csrc/device/rt2_mfma.h",
                                          "raytracing2-fork_amd/csrc/device/rt2_k5_tiles.h",
+                                         "raytracing2-fork_amd/csrc/device/rt2_k5_resident.h",
                                          "raytracing2-fork_amd/csrc/device/rt2_assist.h"],
                                "bvh": ["raytracing2-fork_amd/csrc/device/rt2_bvh.h"]}
 
@@ -236,11 +237,6 @@ def roofline(tests, visits, kern_ms, segments=0, n_tris=0, variant=None):
         rf.update({"bound": "mfma", "achieved": round(mf, 3), "peak": MFMA_F16_PEAK_TFLOPS,
                    "frac": round(mf / MFMA_F16_PEAK_TFLOPS, 4),
                    "pairs_per_s": float(f"{pairs / (kern_ms * 1e-3):.4e}"),
-                   "matrix_pipe_sustained": {"value": MFMA_F16_SUSTAINED_TFLOPS, "unit": "TFLOP/s",
-                                             "frac_of_peak": round(MFMA_F16_SUSTAINED_TFLOPS / MFMA_F16_PEAK_TFLOPS, 3),
-                                             "note": "v_mfma_f32_32x32x16_f16 alone on random f16 operands, 2-4 waves "
-                                                     "per SIMD (scripts/overlap_probe.hip, profiles/r03_overlap_probe"
-                                                     ".jsonl): the clock holds at ~1.2 GHz under that load"},
                    "flop_model": model + "; rays = segments (the active lanes) on the matrix cores",
                    "valu_algorithmic": {"achieved": round(flops, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                                         "frac": round(flops / VALU_PEAK_TFLOPS, 4),
@@ -272,6 +268,15 @@ def attach_traffic(rf, config, variant, kern_ms):
                               f"{prof.get('kernel_variant')} / sources {str(prof.get('kernel_source_sha256'))[:12]}, "
                               f"not this launch ({variant} / {digest[:12]}): traffic not attached")
         return
+    clk = prof.get("clock_ghz")
+    if clk and rf.get("bound") == "mfma":
+        # the dense peak is quoted at 2.4 GHz; the kernel holds a lower clock
+        # under load (DVFS give-back): its own ceiling is peak x clock / 2.4
+        pk = rf["peak"] * clk / MAX_CLOCK_GHZ
+        rf.update({"clock_ghz": round(clk, 3), "peak_at_clock": round(pk, 1),
+                   "frac_at_clock": round(rf["achieved"] / pk, 4),
+                   "clock_source": f"profiles/pmc_config{config}.json: GRBM_GUI_ACTIVE / 8 / kernel ns "
+                                   "(kernel trace of the same --pmc pass)"})
     b = prof.get("hbm_bytes_per_launch")
     if not b:
         return

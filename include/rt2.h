@@ -256,9 +256,18 @@ int rt2_comm_check(rt2_comm* comm);
  * waits for it, not for `stream`); the gather and the un-interleave are then
  * asynchronous on `stream`.  A local failure (a root without d_image, a
  * shard that does not match, no device memory) makes every rank return < 0
- * with nothing issued. */
+ * with nothing issued.  Once the gather is queued, a peer that fails inside
+ * it (ncclCommAbort does not release ranks already in the collective) leaves
+ * `stream` waiting: wait for it with rt2_comm_wait, not an unbounded
+ * hipStreamSynchronize. */
 int rt2_gather_slabs(rt2_comm* comm, const void* d_slab, int32_t width, int32_t height, rt2_shard shard,
                      int32_t root, void* d_image, void* stream);
+/* The host waits for `stream` (e.g. rt2_gather_slabs' gather) under the
+ * RT2_COMM_TIMEOUT_S deadline, polling ncclCommGetAsyncError: 0 when it has
+ * drained; on a timeout, an RCCL error or a stream error the communicator is
+ * aborted as above and < 0 returned (replaces the caller's
+ * hipStreamSynchronize / cudaStreamSynchronize after the collective). */
+int rt2_comm_wait(rt2_comm* comm, void* stream);
 /* The root's un-interleave alone: d_gathered = [nranks][max_rows][width]
  * 16-byte pixels (rank-major slabs, padded to max_rows rows) -> d_image
  * [height][width] for the tile layout {tile_rows, -, nranks}.  Async. */

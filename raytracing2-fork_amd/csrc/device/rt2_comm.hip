@@ -159,6 +159,7 @@ double comm_timeout_s() {
 // transport's: the rank cannot take part in the agreement at all).
 struct RcclTransport {
     rt2_comm* c;
+    double slack_s = 0.0;  // added to the deadline: 2x this rank's own render time (the peers render alike)
     bool usable() const { return c->comm && !c->aborted; }
     bool fault(const char* site) const {
         const char* e = std::getenv("RT2_FAULT_AT");
@@ -182,7 +183,7 @@ struct RcclTransport {
     // never joins it is aborted there instead of blocking forever
     int wait(hipStream_t st) {
         const auto t0 = std::chrono::steady_clock::now();
-        const double limit = comm_timeout_s();
+        const double limit = comm_timeout_s() + slack_s;
         for (;;) {
             const hipError_t q = hipStreamQuery(st);
             if (q == hipSuccess) return 0;
@@ -202,6 +203,21 @@ struct RcclTransport {
             }
             std::this_thread::sleep_for(std::chrono::microseconds(50));
         }
+    }
+    // this rank's own work on stream `st` (no collective in it, so no peer can
+    // hold it up): waited for without a deadline, and its duration becomes
+    // slack on the deadlines that follow — the next agreement also waits for
+    // the slowest peer's render of an equal slab
+    int wait_local(hipStream_t st) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            const hipError_t q = hipStreamQuery(st);
+            if (q == hipSuccess) break;
+            if (q != hipErrorNotReady) return -1;
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
+        slack_s = 2.0 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        return 0;
     }
     // the agreement step: allreduce(max) of two ints on the communicator's own
     // stream, read back into pinned memory and waited for under the deadline;
@@ -344,7 +360,6 @@ extern "C" int rt2_gather_slabs(rt2_comm* c, const void* d_slab, int32_t width, 
         rt2h::set_error("rt2_gather_slabs: bad argument");
         return -1;
     }
-    HIPCHECK(hipSetDevice(c->device));
     hipStream_t st = (hipStream_t)stream;
     const bool is_root = c->rank == root;
     int mr = 0;
@@ -354,6 +369,7 @@ extern "C" int rt2_gather_slabs(rt2_comm* c, const void* d_slab, int32_t width, 
     // this rank's checks, padding and receive buffer: a failure here is agreed
     // on before the gather, so every rank returns < 0 and none issues it
     auto prepare = [&](std::string& err) -> int {
+        if (hipSetDevice(c->device) != hipSuccess) return err = "hipSetDevice failed", -1;
         if (sh.nranks != c->nranks || sh.rank != c->rank || rt2_shard_rows(height, sh) < 0) {
             err = "shard " + std::to_string(sh.rank) + "/" + std::to_string(sh.nranks) +
                   " does not match the communicator's rank " + std::to_string(c->rank) + "/" +
@@ -400,6 +416,20 @@ extern "C" int rt2_gather_slabs(rt2_comm* c, const void* d_slab, int32_t width, 
     return 0;
 }
 
+extern "C" int rt2_comm_wait(rt2_comm* c, void* stream) {
+    if (!c) {
+        rt2h::set_error("rt2_comm_wait: null communicator");
+        return -1;
+    }
+    if (c->aborted) {
+        rt2h::set_error("rt2_comm_wait: the communicator was aborted after a rank-local failure");
+        return -1;
+    }
+    HIPCHECK(hipSetDevice(c->device));
+    RcclTransport t{c};
+    return t.wait((hipStream_t)stream) == 0 ? 0 : -1;  // wait() aborted and set the error
+}
+
 extern "C" int rt2_render_host_gather(rt2_scene* scene, const rt2_uniforms* u, uint32_t frame_begin,
                                       uint32_t frame_count, rt2_shard sh, rt2_comm* c, int32_t root, float* out_rgba,
                                       uint8_t* out_rgb8) {
@@ -425,6 +455,7 @@ extern "C" int rt2_render_host_gather(rt2_scene* scene, const rt2_uniforms* u, u
     }
     const int mr = aerr.empty() ? max_slab_rows(H, sh) : 0, rows = aerr.empty() ? rt2_shard_rows(H, sh) : 0;
     const size_t slab = (size_t)mr * W * 16, whole = aerr.empty() ? (size_t)W * H : 0;
+    RcclTransport t{c};
     auto render = [&](bool rgb8, std::string& err) -> int {
         if (c->acc.ensure(slab) || c->res.ensure(slab) || (rgb8 && c->acc8.ensure(slab)) ||
             (is_root && (c->image.ensure(whole * 16) ||
@@ -440,6 +471,9 @@ extern "C" int rt2_render_host_gather(rt2_scene* scene, const rt2_uniforms* u, u
                        st) != 0 ||
             rt2_resolve_rgba32f((const float*)c->acc.p, (int64_t)rows * W, frame_count, (float*)c->res.p, st) != 0)
             return err = rt2_last_error(), -1;
+        // the render is local: the deadline of agreement 2 starts after it
+        // (a render longer than RT2_COMM_TIMEOUT_S aborted a healthy job)
+        if (t.wait_local(st) != 0) return err = "the render failed on the device", -1;
         return 0;
     };
     auto gathers = [&](bool rgb8) -> int {
@@ -455,7 +489,6 @@ extern "C" int rt2_render_host_gather(rt2_scene* scene, const rt2_uniforms* u, u
         }
         return 0;
     };
-    RcclTransport t{c};
     // the host waits for the whole sequence under the deadline (a peer that
     // fails inside a gather cannot hang this rank), then the root copies out
     auto finish = [&](bool rgb8, std::string& err) -> int {

@@ -266,9 +266,11 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, SH& sh, K5
 // render_mfma's lockstep segment loop around sweep_k5_tiles: every wave of the
 // workgroup takes part in every tile barrier of every segment the workgroup
 // runs (block_any decides, workgroup-uniformly, whether it runs one), sweeping
-// only when it has rays and is not in the cooperative drain.  The path state
-// waits in LDS (lane_stash_packed) across the tile loop in every wave; the
-// launcher takes this kernel only when the packed fields hold the launch.
+// only when it has rays and is not in the cooperative drain.  With lane_lds ==
+// 2 (experiment variants 250/252) the path state waits in LDS
+// (lane_stash_packed) across the tile loop, and the launcher's "llds2" name
+// check keeps those variants to launches the packed fields hold; the default
+// (217, lane_lds == 0) keeps the path state in registers and has no such limit.
 template <MfmaSpec S>
 __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves))) void render_mfma_k5t(RenderParams p_arg) {
     static_assert((S.lane_lds == 2 || (S.lane_lds == 0 && S.rows80)) && S.lockstep, "lockstep segments");

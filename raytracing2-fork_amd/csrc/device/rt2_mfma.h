@@ -80,6 +80,8 @@ struct MfmaSpec {
     bool cthr = false;      // k5 no_tn: the threshold rides in the products' accumulator operand (one matrix
                             // product per group, mfma_thr_frag), and the reduction is a sign-bit AND / OR
                             // (2 v_bitop3_b32 per pair instead of 2.5 min / max)
+    int res_groups = 0;     // render_mfma_k5r (rt2_k5_resident.h): every group's records resident in the
+                            // workgroup's LDS for the whole launch (scenes of <= res_groups 32-triangle groups)
     int sol = 0;            // speed-of-light probes (WRONG images; diag clocks only): 1 = every group reads group
                             // 0's records, 2 = no exact phase, 3 = 2 + only the U term is reduced; marginal-cost
                             // probes (same image): 4 = exact phase twice, 5 = products and reduction twice,
@@ -304,9 +306,8 @@ __device__ __forceinline__ void mfma_main_row(_Float16* row, const f3& d, const 
 
 // mfma_main_row's first K-half only (slots 0..15: d, m.x, m.y, m.z hi), the
 // whole main fragment the forms without -tn read (MfmaSpec::rows80)
-__device__ __forceinline__ void mfma_main_row_half(_Float16* row, const f3& d, const f3& m, float sigma) {
+__device__ __forceinline__ void mfma_main_half_slots(_Float16 s[18], const f3& d, const f3& m, float sigma) {
     const float comp[6] = {d.x, d.y, d.z, m.x, m.y, m.z};
-    _Float16 s[18];
 #pragma unroll
     for (int c = 0; c < 6; c++) {
         const float v = comp[c] * sigma;
@@ -316,6 +317,10 @@ __device__ __forceinline__ void mfma_main_row_half(_Float16* row, const f3& d, c
         s[3 * c + 1] = lo;
         s[3 * c + 2] = hi;
     }
+}
+__device__ __forceinline__ void mfma_main_row_half(_Float16* row, const f3& d, const f3& m, float sigma) {
+    _Float16 s[18];
+    mfma_main_half_slots(s, d, m, sigma);
     h8* r = reinterpret_cast<h8*>(row);
     r[0] = h8{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7]};
     r[1] = h8{s[8], s[9], s[10], s[11], s[12], s[13], s[14], s[15]};
@@ -719,15 +724,19 @@ __device__ __forceinline__ unsigned long long k5_cthr_group(ThrBits tb, const h8
                                                             const h8& b2, const h8& b4, const h8& b6, bool upper,
                                                             const SH& sh) {
     static_assert(S.k5 && S.no_tn && S.sol == 0, "the 4-product form");
-    constexpr int YO = S.rows80 ? 16 : 32;
-    const int r32 = (int)lane_id() & 31, hl = (int)lane_id() >> 5;
+    [[maybe_unused]] constexpr int YO = S.rows80 ? 16 : 32;
+    [[maybe_unused]] const int r32 = (int)lane_id() & 31, hl = (int)lane_id() >> 5;
     const f16v zero = {};
     const f16v TT = __builtin_amdgcn_mfma_f32_32x32x16_f16(mfma_thr_frag(tb), b6, zero, 0, 0, 0);
     int acc = 0;
 #pragma unroll
     for (int R = 0; R < 2; R++) {
         if (R == 1 && !upper) break;
-        const h8 aR = S.ylds == 2 ? *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][8 * hl]) : a0[R];
+        h8 aR;
+        if constexpr (S.ylds == 2)
+            aR = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][8 * hl]);
+        else
+            aR = a0[R];
         const f16v U = __builtin_amdgcn_mfma_f32_32x32x16_f16(aR, b0, TT, 0, 0, 0);
         const f16v V = __builtin_amdgcn_mfma_f32_32x32x16_f16(aR, b2, TT, 0, 0, 0);
         const f16v X = __builtin_amdgcn_mfma_f32_32x32x16_f16(aR, b4, TT, 0, 0, 0);
@@ -737,7 +746,11 @@ __device__ __forceinline__ unsigned long long k5_cthr_group(ThrBits tb, const h8
         for (int i = 0; i < 16; i++)  // U & V & X (LUT index 4 S0 + 2 S1 + S2)
             t3[i] = __builtin_amdgcn_bitop3_b32(__float_as_int(U[i]), __float_as_int(V[i]), __float_as_int(X[i]), 0x80);
         __builtin_amdgcn_sched_barrier(0);
-        const h8 yR = S.ylds ? *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][YO + 8 * hl]) : y1[R];
+        h8 yR;
+        if constexpr (S.ylds != 0)
+            yR = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][YO + 8 * hl]);
+        else
+            yR = y1[R];
         const f16v Y = __builtin_amdgcn_mfma_f32_32x32x16_f16(yR, b6, TT, 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll

@@ -39,8 +39,7 @@ using namespace rt2d;
 #include "rt2_brute.h"
 #include "rt2_mfma.h"
 #include "rt2_k5_tiles.h"
-#include "rt2_k5_pool.h"
-#include "rt2_k5_dtiles.h"
+#include "rt2_k5_resident.h"
 #include "rt2_assist.h"
 #include "rt2_bvh.h"
 #include "rt2_misc_kernels.h"
@@ -612,6 +611,22 @@ constexpr MfmaSpec k5_tiles_spec(int K, bool no_tn, int tail, bool diag = false)
     x.diag = diag;
     return x;
 }
+// records resident in LDS (rt2_k5_resident.h): one workgroup per CU (3 or 4
+// waves per SIMD), scenes of <= kResGroups 32-triangle groups
+constexpr int kResGroups = 38;  // 152 KiB of k5 records (4 KiB per group) of the CU's 160 KiB
+constexpr MfmaSpec k5_res_spec(int waves, bool prefetch, bool diag = false) {
+    MfmaSpec x = kMfmaK5NoTn;
+    x.block = 256 * waves;
+    x.waves = waves;
+    x.tail_lanes = 4;
+    x.lane_lds = 0;
+    x.cthr = true;
+    x.lockstep = false;
+    x.prefetch = prefetch;
+    x.res_groups = kResGroups;
+    x.diag = diag;
+    return x;
+}
 constexpr Bvh3Spec kBvhDefault{.block = 256, .thresh = 16, .slab = Slab::Markstein, .waves = 5, .diag = false};
 
 #ifdef RT2_EXPERIMENTS
@@ -679,9 +694,15 @@ const Variant kVariants[] = {
     // LDS record tiles shared by the workgroup (rt2_k5_tiles.h; DESIGN.md "LDS record tiles"), the default above
     // 8,192 triangles: 10-group tiles, path state in registers, the threshold in the accumulator
     RT2_VARIANT(217, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(10, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile10/coop0/w3/cmp/rows80/regs/cthr"),
+    // scenes of <= 38 groups (1,216 triangles: config B): every group's records resident in LDS for the whole
+    // launch (rt2_k5_resident.h), fragments built in registers by v_permlane32_swap, waves run free
+    RT2_VARIANT(280, K_MFMA, render_mfma_k5r<k5_res_spec(3, false)>, 768, "mfmar/768/k5/notn/res38/coop4/w3/cmp/cthr"),
+    RT2_VARIANT(281, K_MFMA, render_mfma_k5r<k5_res_spec(3, true)>, 768, "mfmar/768/k5/notn/res38/coop4/w3/cmp/cthr/pf"),
+    RT2_VARIANT(282, K_MFMA, render_mfma_k5r<k5_res_spec(4, false)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr"),
+    RT2_VARIANT(283, K_MFMA, render_mfma_k5r<k5_res_spec(4, true)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/pf"),
 #ifdef RT2_EXPERIMENTS
-    // earlier product kernels (round 2's 16x16x32 form; round 3's k16 sweep and 5-product choices; round 4's
-    // first tile forms and the small-scene kernels before the threshold moved into the accumulator), kept for A/B
+    // earlier choices of rounds 3-4 (the 5-product form before and after the threshold moved into the accumulator,
+    // the first tile forms), kept for A/B; rounds 2-3's 16x16x32 and k16 kernels are in git history
     RT2_VARIANT(231, K_MFMA, render_mfma<kMfmaK5NoTn>, 256, "mfma/256/k5/notn/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"),
     RT2_VARIANT(243, K_MFMA, render_mfma<kMfmaK5NoTnW4C4>, 256, "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
     RT2_VARIANT(213, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(10, true, 0); x.rows80 = true; x.lane_lds = 0; return x; }()>, 768, "mfmat5/768/k5/notn/tile10/coop0/w3/cmp/rows80/regs"),
@@ -689,141 +710,20 @@ const Variant kVariants[] = {
     RT2_VARIANT(228, K_MFMA, render_mfma<kMfmaK5W4>, 256, "mfma/256/k5/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
     RT2_VARIANT(233, K_MFMA, render_mfma<kMfmaK5NoTnW4>, 256, "mfma/256/k5/notn/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
     RT2_VARIANT(250, K_MFMA, render_mfma_k5t<k5_tiles_spec(4, false, 0)>, 768, "mfmat5/768/k5/tile4/coop0/w3/llds2/cmp"),
-    RT2_VARIANT(152, K_MFMA, render_mfma<kMfmaT8Y4>, 256, "mfma/256/f16x3/coop8/w4/imax/minred/ymma/t12"),
-    RT2_VARIANT(150, K_MFMA, render_mfma<kMfmaT8Y>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma/t12"),
-    RT2_VARIANT(200, K_MFMA, render_mfma<kMfmaK16>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"),
-    RT2_VARIANT(206, K_MFMA, render_mfma<kMfmaK16W4>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
-    RT2_VARIANT(244, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4C4; x.dpp = true; return x; }()>, 256, "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp/dpp"),
-    RT2_VARIANT(255, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(4, true, 0); x.dpp = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile4/coop0/w3/llds2/cmp/dpp"),
-    RT2_VARIANT(256, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(8, true, 0); x.block = 512; x.waves = 2; return x; }()>, 512, "mfmat5/512/k5/notn/tile8/coop0/w2/llds2/cmp"),
-    RT2_VARIANT(257, K_MFMA, render_mfma_k5t<k5_tiles_spec(4, true, 4)>, 768, "mfmat5/768/k5/notn/tile4/coop4/w3/llds2/cmp"),
-    RT2_VARIANT(237, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(4, true, 0); x.rows80 = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile4/coop0/w3/llds2/cmp/rows80"),
-    RT2_VARIANT(249, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(4, true, 0); x.rows80 = true; x.tile_bufs = 3; return x; }()>, 768, "mfmat5/768/k5/notn/tile4x3/coop0/w3/llds2/cmp/rows80"),
-    RT2_VARIANT(238, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(6, true, 0); x.rows80 = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile6/coop0/w3/llds2/cmp/rows80"),
-    RT2_VARIANT(214, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(10, true, 0); x.rows80 = true; x.lane_lds = 0; x.prefetch = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile10/coop0/w3/cmp/rows80/regs/pf"),
-    RT2_VARIANT(215, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(10, true, 8); x.rows80 = true; x.lane_lds = 0; return x; }()>, 768, "mfmat5/768/k5/notn/tile10/coop8/w3/cmp/rows80/regs"),
     RT2_VARIANT(260, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4C4; x.cthr = true; return x; }()>, 256, "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp/cthr"),
     RT2_VARIANT(261, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4C4; x.cthr = true; x.ylds = 2; return x; }()>, 256, "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp/cthr/ylds"),
-    RT2_VARIANT(269, K_MFMA, render_mfma_k5d<[] { MfmaSpec x = k5_tiles_spec(10, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; return x; }()>, 768, "mfmat5d/768/k5/notn/tile10/coop0/w3/cmp/rows80/regs/cthr/dec"),
-    RT2_VARIANT(270, K_MFMA, render_mfma_k5d<[] { MfmaSpec x = k5_tiles_spec(6, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; return x; }()>, 768, "mfmat5d/768/k5/notn/tile6/coop0/w3/cmp/rows80/regs/cthr/dec"),
-    RT2_VARIANT(216, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(11, true, 0); x.rows80 = true; x.lane_lds = 0; return x; }()>, 768, "mfmat5/768/k5/notn/tile11/coop0/w3/cmp/rows80/regs"),
     RT2_VARIANT(212, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(8, true, 0); x.rows80 = true; x.lane_lds = 0; return x; }()>, 768, "mfmat5/768/k5/notn/tile8/coop0/w3/cmp/rows80/regs"),
-    RT2_VARIANT(258, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(4, true, 0); x.prefetch = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile4/coop0/w3/llds2/cmp/pf"),
-    RT2_VARIANT(259, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(4, true, 0); x.prefetch = true; x.dpp = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile4/coop0/w3/llds2/cmp/pf/dpp"),
-    RT2_VARIANT(245, K_MFMA, render_mfma_pool<[] { MfmaSpec x = kMfmaK5NoTnW4C4; x.rows80 = true; x.wg_pool = true; return x; }()>, 256, "mfmap/256/k5/notn/coop4/w4/llds2/rows80/pool"),
-    RT2_VARIANT(247, K_MFMA, render_mfma_pool<[] { MfmaSpec x = kMfmaK5NoTnW4C4; x.rows80 = true; x.wg_pool = true; x.wg_split = true; return x; }()>, 256, "mfmap/256/k5/notn/coop4/w4/llds2/rows80/pool/split"),
-    RT2_VARIANT(248, K_MFMA, render_mfma_pool<[] { MfmaSpec x = kMfmaK5NoTnW4C4; x.rows80 = true; x.wg_pool = true; x.wg_split = true; x.tail_lanes = 0; return x; }()>, 256, "mfmap/256/k5/notn/coop0/w4/llds2/rows80/pool/split"),
     RT2_VARIANT(246, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4C4; x.rows80 = true; return x; }()>, 256, "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp/rows80"),
     RT2_VARIANT(251, K_MFMA, render_mfma_k5t<k5_tiles_spec(4, false, 0, true)>, 768, "mfmat5/768/k5/tile4/coop0/w3/llds2/cmp/diag"),
-    RT2_VARIANT(253, K_MFMA, render_mfma_k5t<k5_tiles_spec(2, false, 0)>, 768, "mfmat5/768/k5/tile2/coop0/w3/llds2/cmp"),
-    RT2_VARIANT(254, K_MFMA, render_mfma_k5t<k5_tiles_spec(4, false, 8)>, 768, "mfmat5/768/k5/tile4/coop8/w3/llds2/cmp"),
-    RT2_VARIANT(160, K_MFMA, render_mfma<k16_spec(3)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12"),
-    RT2_VARIANT(161, K_MFMA, render_mfma<k16_spec(4)>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12"),
-    RT2_VARIANT(162, K_MFMA, render_mfma<k16_spec(2)>, 256, "mfma/256/k16/coop8/w2/imax/minred/ymma/t12"),
-    RT2_VARIANT(163, K_MFMA, render_mfma<k16_spec(4, true)>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/alds"),
-    RT2_VARIANT(164, K_MFMA, render_mfma<k16_spec(3, true)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/alds"),
-    RT2_VARIANT(165, K_MFMA, render_mfma<k16_spec(3, false, true)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/diag"),
-    RT2_VARIANT(169, K_MFMA, render_mfma<kMfmaT8Y4D>, 256, "mfma/256/f16x3/coop8/w4/imax/minred/ymma/t12/diag"),  // 152 + diag
-    RT2_VARIANT(170, K_MFMA, render_mfma<k16_spec(2, false, false, false, true)>, 256, "mfma/256/k16/coop8/w2/imax/minred/ymma/t12/pf"),
-    RT2_VARIANT(171, K_MFMA, render_mfma<k16_spec(3, false, false, false, true)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/pf"),
-    RT2_VARIANT(172, K_MFMA, render_mfma<k16_spec(3, true, false, false, true)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/alds/pf"),
-    RT2_VARIANT(173, K_MFMA, render_mfma<k16_spec(2, true, false, false, true)>, 256, "mfma/256/k16/coop8/w2/imax/minred/ymma/t12/alds/pf"),
-    RT2_VARIANT(174, K_MFMA, render_mfma<k16_spec(3, false, true, false, true)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/pf/diag"),
-    RT2_VARIANT(190, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3, false, true); x.sol = 1; return x; }()>, 256, "SOL1/k16/w3/records-of-group-0"),
-    RT2_VARIANT(191, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3, false, true); x.sol = 2; return x; }()>, 256, "SOL2/k16/w3/no-exact-phase"),
-    RT2_VARIANT(192, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3, false, true); x.sol = 3; return x; }()>, 256, "SOL3/k16/w3/U-only"),
-    RT2_VARIANT(175, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3); x.lane_lds = true; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds"),
-    RT2_VARIANT(176, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3, false, false, false, true); x.lane_lds = true; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/pf/llds"),
-    RT2_VARIANT(177, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(4); x.lane_lds = true; return x; }()>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/llds"),
-    RT2_VARIANT(178, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(4, true); x.lane_lds = true; return x; }()>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/alds/llds"),
-    RT2_VARIANT(179, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(4, true); x.lane_lds = true; x.serial = 1; return x; }()>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/alds/llds/ser1"),
-    RT2_VARIANT(180, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(4, true); x.lane_lds = true; x.serial = 2; return x; }()>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/alds/llds/ser2"),
-    RT2_VARIANT(181, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3); x.serial = 1; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/ser1"),
-    RT2_VARIANT(182, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3); x.serial = 2; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/ser2"),
-    RT2_VARIANT(183, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(4); x.serial = 1; return x; }()>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/ser1"),
-    RT2_VARIANT(184, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3, false, false, false, true); x.lane_lds = true; x.serial = 1; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/pf/llds/ser1"),
-    RT2_VARIANT(189, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3); x.lane_lds = true; x.serial = 1; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser1"),
-    RT2_VARIANT(193, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3, true, false, false, true); x.lane_lds = true; x.serial = 1; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/alds/pf/llds/ser1"),
-    RT2_VARIANT(194, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3, true); x.serial = 1; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/alds/ser1"),
-    RT2_VARIANT(195, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3); x.lane_lds = true; x.serial = 1; x.sol = 4; return x; }()>, 256, "SOL4/k16/llds/ser1/exact-phase-twice"),
-    RT2_VARIANT(196, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3); x.lane_lds = true; x.serial = 1; x.sol = 5; return x; }()>, 256, "SOL5/k16/llds/ser1/products-and-reduction-twice"),
-    RT2_VARIANT(197, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3); x.lane_lds = true; x.serial = 3; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser3"),
-    RT2_VARIANT(198, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3); x.lane_lds = true; x.serial = 4; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser4"),
-    RT2_VARIANT(199, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(2); x.lane_lds = true; x.serial = 4; return x; }()>, 256, "mfma/256/k16/coop8/w2/imax/minred/ymma/t12/llds/ser4"),
-    RT2_VARIANT(202, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.lateload = true; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp/ll"),
-    RT2_VARIANT(203, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.lateload = true; x.serial = 1; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser1/cmp/ll"),
-    RT2_VARIANT(204, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.waves = 4; x.lane_lds = 2; x.afrag_lds = true; return x; }()>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/alds/llds2/ser4/cmp"),
-    RT2_VARIANT(205, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.lane_lds = 2; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds2/ser4/cmp"),
-    RT2_VARIANT(207, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.sol = 1; return x; }()>, 256, "SOL1/k16/200/records-of-group-0"),
-    RT2_VARIANT(208, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.tshift = 10; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t10/llds/ser4/cmp"),
-    RT2_VARIANT(209, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.tshift = 8; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t8/llds/ser4/cmp"),
-    RT2_VARIANT(210, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.diag = true; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp/diag"),
-    RT2_VARIANT(211, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.diag = true; x.tshift = 8; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t8/llds/ser4/cmp/diag"),
-    RT2_VARIANT(222, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16W4; x.diag = true; return x; }()>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp/diag"),
-    // the 5-product form (MfmaSpec::k5): U, -V, X from the first K-half, the m.z residual bounded in the threshold
-    RT2_VARIANT(234, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4; x.serial = 1; return x; }()>, 256, "mfma/256/k5/notn/coop8/w4/imax/minred/ymma/t12/llds2/ser1/cmp"),
-    RT2_VARIANT(235, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4; x.serial = 3; return x; }()>, 256, "mfma/256/k5/notn/coop8/w4/imax/minred/ymma/t12/llds2/ser3/cmp"),
-    RT2_VARIANT(236, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4; x.compact = false; return x; }()>, 256, "mfma/256/k5/notn/coop8/w4/imax/minred/ymma/t12/llds2/ser4"),
-    RT2_VARIANT(240, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4; x.tail_lanes = 4; return x; }()>, 256, "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
-    RT2_VARIANT(241, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4; x.tail_lanes = 16; return x; }()>, 256, "mfma/256/k5/notn/coop16/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
-    RT2_VARIANT(242, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4; x.tail_lanes = 0; return x; }()>, 256, "mfma/256/k5/notn/coop0/w4/imax/minred/ymma/t12/llds2/ser4/cmp"),
+    // diagnostic builds (group / survivor / exact-test counters, wave timeline)
     RT2_VARIANT(239, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTnW4; x.diag = true; return x; }()>, 256, "mfma/256/k5/notn/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp/diag"),
     RT2_VARIANT(232, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5NoTn; x.diag = true; return x; }()>, 256, "mfma/256/k5/notn/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp/diag"),
     RT2_VARIANT(229, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5; x.diag = true; return x; }()>, 256, "mfma/256/k5/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp/diag"),
-    RT2_VARIANT(230, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK5; x.waves = 4; return x; }()>, 256, "mfma/256/k5/coop8/w4/imax/minred/ymma/t12/llds/ser4/cmp"),
-    // the k16 kernels without the workgroup's per-segment barrier (waves run free)
-    RT2_VARIANT(223, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.lockstep = false; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp/free"),
-    RT2_VARIANT(224, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16W4; x.lockstep = false; return x; }()>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp/free"),
-    RT2_VARIANT(225, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.lockstep = false; x.diag = true; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp/free/diag"),
-    RT2_VARIANT(226, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16W4; x.lockstep = false; x.diag = true; return x; }()>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/llds2/ser4/cmp/free/diag"),
-    RT2_VARIANT(218, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.sol = 6; return x; }()>, 256, "SOL6/k16/200/reduction-VALU-twice"),
-    RT2_VARIANT(219, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.sol = 7; return x; }()>, 256, "SOL7/k16/200/products-twice"),
-    RT2_VARIANT(220, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.sol = 5; return x; }()>, 256, "SOL5/k16/200/products-and-reduction-twice"),
-    RT2_VARIANT(221, K_MFMA, render_mfma<[] { MfmaSpec x = kMfmaK16; x.sol = 4; return x; }()>, 256, "SOL4/k16/200/exact-phase-twice"),
-    RT2_VARIANT(201, K_MFMA, render_mfma<[] { MfmaSpec x = k16_spec(3); x.lane_lds = true; x.serial = 1; x.compact = true; return x; }()>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/llds/ser1/cmp"),
-    RT2_VARIANT(166, K_MFMA, render_mfma<k16_spec(3, false, false, true)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/rsplit"),
-    RT2_VARIANT(167, K_MFMA, render_mfma<k16_spec(4, true, false, true)>, 256, "mfma/256/k16/coop8/w4/imax/minred/ymma/t12/alds/rsplit"),
-    RT2_VARIANT(168, K_MFMA, render_mfma<k16_spec(3, true, false, true)>, 256, "mfma/256/k16/coop8/w3/imax/minred/ymma/t12/alds/rsplit"),
-    RT2_VARIANT(140, K_MFMA, render_mfma<kMfmaT8>, 256, "mfma/256/f16x3/coop8/w2/imax/minred"),  // Y by one FMA per pair
-    RT2_VARIANT(137, K_MFMA, render_mfma<kMfmaIM>, 256, "mfma/256/f16x3/coop16/w2/imax/minred"),  // drain at 16 live rays
-    RT2_VARIANT(143, K_MFMA, render_mfma<kMfmaT4>, 256, "mfma/256/f16x3/coop4/w2/imax/minred"),
-    RT2_VARIANT(144, K_MFMA, render_mfma<kMfmaT0>, 256, "mfma/256/f16x3/coop0/w2/imax/minred"),
-    RT2_VARIANT(145, K_MFMA, render_mfma<kMfmaT8F>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/free"),
-    RT2_VARIANT(147, K_MFMA, render_mfma<kMfmaT8D>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/diag"),  // 140 + counters
-    RT2_VARIANT(151, K_MFMA, render_mfma<kMfmaT8YD>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma/diag"),
-    RT2_VARIANT(153, K_MFMA, render_mfma<kMfmaT8Y3>, 256, "mfma/256/f16x3/coop8/w3/imax/minred/ymma"),
-    RT2_VARIANT(154, K_MFMA, render_mfma<kMfmaT8Y4T10>, 256, "mfma/256/f16x3/coop8/w4/imax/minred/ymma/t10"),  // T = 2^-10 R0
-    RT2_VARIANT(155, K_MFMA, render_mfma<kMfmaT8Y4T14>, 256, "mfma/256/f16x3/coop8/w4/imax/minred/ymma/t14"),  // below the proven margin
-    RT2_VARIANT(156, K_MFMA, render_mfma<kMfmaT8YDT12>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma/t12/diag"),
-    RT2_VARIANT(157, K_MFMA, render_mfma<kMfmaT8Y2W>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma/t12/occ2"),
-    RT2_VARIANT(158, K_MFMA, render_mfma<kMfmaT8Y1W>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/ymma/t12/occ1"),
-    RT2_VARIANT(148, K_MFMA, render_mfma<kMfmaT8P3>, 256, "mfma/256/f16x3/coop8/w3/imax/minred/pf"),  // 140 + prefetch, 3 waves
-    RT2_VARIANT(149, K_MFMA, render_mfma<kMfmaT8P2>, 256, "mfma/256/f16x3/coop8/w2/imax/minred/pf"),  // 140 + prefetch
-    RT2_VARIANT(146, K_MFMA, render_mfma<kMfmaT4F>, 256, "mfma/256/f16x3/coop4/w2/imax/minred/free"),
-    RT2_VARIANT(138, K_MASSIST, render_assist<kAssistM>, 768, "massist12/f16x3/w3/imax"),
-    RT2_VARIANT(139, K_MASSIST, render_assist<kAssistMM>, 768, "massist12/f16x3/w3/imax/minred"),
-    RT2_VARIANT(131, K_MFMA, render_mfma<kMfmaI>, 256, "mfma/256/f16x3/coop16/w2/imax"),      // a compare per pair
-    RT2_VARIANT(130, K_MFMA, render_mfma<kMfmaDefault>, 256, "mfma/256/f16x3/coop16/w2"),      // f32 max (NaN quieting)
-    RT2_VARIANT(132, K_MFMA, render_mfma<kMfmaIP>, 256, "mfma/256/f16x3/coop16/w2/imax/pf"),
-    RT2_VARIANT(133, K_MFMA, render_mfma<kMfmaP>, 256, "mfma/256/f16x3/coop16/w2/pf"),
-    RT2_VARIANT(134, K_MFMA, render_mfma<kMfmaI4>, 256, "mfma/256/f16x3/coop16/w4/imax"),
-    RT2_VARIANT(135, K_MFMA, render_mfma<kMfmaIP4>, 256, "mfma/256/f16x3/coop16/w4/imax/pf"),
+    // scalar-path and BVH kernels of rounds 1-2 (DESIGN.md "Tried and measured"; parity-tested in the experiment build)
     RT2_VARIANT(67, K_SMEM, render_smem<kSmemMid>, 256, "smem/256/max3f8/coop32"),         // round-1 choice, 1-4 items per lane
     RT2_VARIANT(85, K_SPLIT, render_split<kSplitSmall>, 256, "split4/max3f8/w6"),          // round-1 choice, < 1 item per lane
-    RT2_VARIANT(90, K_ASSIST, render_assist<kAssist8>, 512, "assist8/max3f8/w6"),
-    RT2_VARIANT(95, K_ASSIST, render_assist<assist12_x(48)>, 768, "assist12/max3f8/w6/coop48"),
     RT2_VARIANT(53, K_BVH3, render_bvh3<kBvhDefault>, 256, "bvh3/256/t16/w5"),            // round-1/2 BVH default
-    RT2_VARIANT(101, K_SMEM, render_smem<kSmemLock512>, 512, "smem/512/max3f8/coop32/w6/lockstep"),
-    RT2_VARIANT(104, K_SMEM, render_smem<kSmemLock128>, 128, "smem/128/max3f8/coop32/w6/lockstep"),
     RT2_VARIANT(106, K_SMEM, render_smem<kSmemFree>, 256, "smem/256/max3f8/coop32/w6/free"),  // round-1 default
-    RT2_VARIANT(97, K_ASSIST, render_assist<assist12_x(16)>, 768, "assist12/max3f8/w6/coop16"),
-    RT2_VARIANT(22, K_RESIDENT, (render_resident<ResidentSpec{512, 8, Filter::Five}>), 512, "resident/512/masked8"),
-    RT2_VARIANT(24, K_SMEM, render_smem<smem_x(8, Filter::Five, Tail::None, 0, 1)>, 256, "smem/256/masked8"),
-    RT2_VARIANT(26, K_TILED, (render_tiled<TiledSpec{512, 4, Filter::Five}>), 512, "tiled/512/masked4"),
-    RT2_VARIANT(27, K_SMEM, render_smem<smem_x(8, Filter::Five, Tail::Coop, 16, 1)>, 256, "smem/256/masked8/coop16"),
-    RT2_VARIANT(28, K_SMEM, render_smem<smem_x(8, Filter::Five, Tail::Coop, 32, 1)>, 256, "smem/256/masked8/coop32"),
-    RT2_VARIANT(29, K_SMEM, render_smem<smem_x(8, Filter::Five, Tail::Coop, 48, 1)>, 256, "smem/256/masked8/coop48"),
-    RT2_VARIANT(30, K_SMEM, render_smem<smem_x(8, Filter::Five, Tail::Coop, 64, 1)>, 256, "smem/256/masked8/coop64"),
     RT2_VARIANT(37, K_BVH, render_bvh<BvhSpec{256}>, 256, "bvh/256"),
     RT2_VARIANT(40, K_BVH2, (render_bvh2<Bvh2Spec{256, 16}>), 256, "bvh2/256/t16"),
     RT2_VARIANT(41, K_BVH2, (render_bvh2<Bvh2Spec{256, 8}>), 256, "bvh2/256/t8"),
@@ -833,29 +733,17 @@ const Variant kVariants[] = {
     RT2_VARIANT(47, K_BVH3, render_bvh3<bvh3_x(8, Slab::Markstein, 1)>, 256, "bvh3/256/t8"),
     RT2_VARIANT(48, K_BVH3, render_bvh3<bvh3_x(24, Slab::Markstein, 1)>, 256, "bvh3/256/t24"),
     RT2_VARIANT(50, K_BVH3, render_bvh3<bvh3_x(16, Slab::Binary64, 1)>, 256, "bvh3/256/t16/div64"),
-    RT2_VARIANT(52, K_SMEM, render_smem<smem_x(8, Filter::Five, Tail::Coop, 32, 6)>, 256, "smem/256/masked8/coop32/w6"),
     RT2_VARIANT(54, K_BVH3, render_bvh3<bvh3_x(8, Slab::Markstein, 5)>, 256, "bvh3/256/t8/w5"),
     RT2_VARIANT(55, K_BVH3, render_bvh3<bvh3_x(16, Slab::Filtered, 5)>, 256, "bvh3/256/t16/filt/w5"),
     RT2_VARIANT(58, K_BVH3, render_bvh3<bvh3_x(16, Slab::Markstein, 5, true)>, 256, "bvh3/256/t16/w5/DIAG"),
     RT2_VARIANT(64, K_SMEM, render_smem<smem_x(8, Filter::Five, Tail::Team, 32, 1)>, 256, "smem/256/masked8/team32"),
-    RT2_VARIANT(65, K_SMEM, render_smem<smem_x(8, Filter::Five, Tail::Team, 48, 1)>, 256, "smem/256/masked8/team48"),
     RT2_VARIANT(66, K_SMEM, render_smem<smem_x(8, Filter::Five, Tail::Team, 64, 1)>, 256, "smem/256/masked8/team64"),
-    RT2_VARIANT(68, K_SMEM, render_smem<smem_x(4, Filter::Max3, Tail::Coop, 32, 1)>, 256, "smem/256/max3f4/coop32"),
-    RT2_VARIANT(70, K_SPLIT, render_split<split_x(2, Filter::Five, 5)>, 128, "split2/masked8/w5"),
-    RT2_VARIANT(71, K_SPLIT, render_split<split_x(4, Filter::Five, 5)>, 256, "split4/masked8/w5"),
-    RT2_VARIANT(72, K_SPLIT, render_split<split_x(2, Filter::Max3, 5)>, 128, "split2/max3f8/w5"),
-    RT2_VARIANT(73, K_SPLIT, render_split<split_x(4, Filter::Max3, 5)>, 256, "split4/max3f8/w5"),
     RT2_VARIANT(74, K_SMEM, render_smem<smem_x(4, Filter::Plk, Tail::Coop, 32, 1)>, 256, "smem/256/plk4/coop32"),
     RT2_VARIANT(76, K_SMEM, render_smem<smem_x(8, Filter::Plk, Tail::Coop, 32, 1)>, 256, "smem/256/plk8/coop32"),
     RT2_VARIANT(79, K_SMEM, render_smem<smem_x(8, Filter::Plk, Tail::Coop, 32, 6)>, 256, "smem/256/plk8/coop32/w6"),
     RT2_VARIANT(80, K_SMEM, render_smem<smem_x(2, Filter::Plk, Tail::Coop, 32, 1)>, 256, "smem/256/plk2/coop32"),
-    RT2_VARIANT(81, K_SMEM, render_smem<smem_x(4, Filter::Plk, Tail::Coop, 32, 1, true)>, 256,
-                "smem/256/plk4/coop32/STATS"),
     RT2_VARIANT(82, K_SMEM, render_smem<smem_x(8, Filter::Max3, Tail::Coop, 32, 1, true)>, 256,
                 "smem/256/max3f8/coop32/STATS"),
-    RT2_VARIANT(84, K_SPLIT, render_split<split_x(8, Filter::Max3, 4)>, 512, "split8/max3f8/w4"),
-    RT2_VARIANT(87, K_TILED, (render_tiled<TiledSpec{512, 8, Filter::Max3}>), 512, "tiled/512/max3f8"),
-    RT2_VARIANT(89, K_TILED, (render_tiled<TiledSpec{1024, 4, Filter::Max3}>), 1024, "tiled/1024/max3f4"),
 #endif
 };
 constexpr size_t kResidentMaxBytes = 112 * 1024;
@@ -1096,9 +984,15 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
             p.order = s->d_order;
             p.n_runs = (uint32_t)runs;
         }
-        p.cost_out = s->d_cost;
-        s->cost_npix = p.n_pix;
-        std::memcpy(s->cost_key, key, sizeof(key));
+        // the cost map keeps each item's start clock in the pixel's own slot:
+        // with frame-major items several frames of one pixel run at once and
+        // would share it, so only whole-pixel launches measure
+        // (frame-split launches still use the order of an earlier map)
+        if (!p.frame_split) {
+            p.cost_out = s->d_cost;
+            s->cost_npix = p.n_pix;
+            std::memcpy(s->cost_key, key, sizeof(key));
+        }
     }
     const size_t resident_bytes = (size_t)3 * sizeof(float4) * (size_t)std::max(s->n_tris, 1);
     const bool fits = resident_bytes <= kResidentMaxBytes;
@@ -1110,6 +1004,8 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     const Variant* VP = s->variant > 0 ? find_variant(s->variant) : nullptr;
     if (VP && ((s->traversal == RT2_TRAVERSAL_BVH) != is_bvh(VP->kind))) VP = nullptr;
     if (VP && VP->kind == K_RESIDENT && !fits) VP = nullptr;  // cannot hold this scene
+    const bool res_fits = (s->n_tris + 31) / 32 <= kResGroups;  // render_mfma_k5r's LDS holds every record group
+    if (VP && !res_fits && std::strncmp(VP->name, "mfmar/", 6) == 0) VP = nullptr;
     if (VP && (VP->kind == K_MFMA || VP->kind == K_MASSIST) && !s->mfma_ok) VP = nullptr;  // scene outside the filter's range
     // the packed path state (lane_lds = 2) holds 16-bit x, y, rays per pixel and 12-bit bounce counts
     const bool packed = u->width <= 65535 && u->height <= 65535 && u->maxBounceCount <= 4095 &&

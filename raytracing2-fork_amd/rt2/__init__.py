@@ -169,6 +169,7 @@ EXPORTED = [
     "rt2_uniforms_offline", "rt2_write_png", "rt2_image_load", "rt2_image_free", "rt2_sd_texture",
     "rt2_scene_set_textures", "rt2_comm_unique_id", "rt2_comm_init", "rt2_comm_wrap", "rt2_comm_destroy",
     "rt2_comm_size", "rt2_comm_check", "rt2_gather_slabs", "rt2_unshard_slabs", "rt2_render_host_gather",
+    "rt2_comm_wait",
 ]
 
 _lib: Optional[C.CDLL] = None
@@ -258,6 +259,7 @@ def lib() -> C.CDLL:
         "rt2_comm_destroy": (None, [P]),
         "rt2_comm_size": (C.c_int, [P, C.POINTER(I32), C.POINTER(I32)]),
         "rt2_comm_check": (C.c_int, [P]),
+        "rt2_comm_wait": (C.c_int, [P, P]),
         "rt2_gather_slabs": (C.c_int, [P, P, I32, I32, Shard, I32, P, P]),
         "rt2_unshard_slabs": (C.c_int, [P, I32, I32, I32, Shard, P, P]),
         "rt2_render_host_gather": (C.c_int, [P, C.POINTER(Uniforms), U32, U32, Shard, P, I32, P, P]),
@@ -481,6 +483,10 @@ class Comm:
         _check(lib().rt2_gather_slabs(self._p, C.c_void_p(slab_ptr), width, height, sh, root,
                                       C.c_void_p(image_ptr) if image_ptr else None,
                                       C.c_void_p(stream) if stream else None), "rt2_gather_slabs")
+
+    def wait(self, stream: int = 0) -> None:
+        """rt2_comm_wait: the stream drained under the RT2_COMM_TIMEOUT_S deadline."""
+        _check(lib().rt2_comm_wait(self._p, C.c_void_p(stream) if stream else None), "rt2_comm_wait")
 
 
 def unshard_slabs(gathered_ptr: int, max_rows: int, width: int, height: int, layout: Shard, image_ptr: int,

@@ -63,7 +63,9 @@ def main(config="B"):
     if durs:
         out["kernel_ns_profiled"] = sum(durs) / len(durs)
         if "GRBM_GUI_ACTIVE" in res:
-            out["effective_clock_ghz"] = res["GRBM_GUI_ACTIVE"] / 8 / out["kernel_ns_profiled"]
+            # the clock the kernel held (MI355X_MICROARCH.md "DVFS give-back": GRBM_GUI_ACTIVE sums the 8
+            # XCDs); bench.py prices the matrix roofline at this clock beside the 2.4 GHz spec
+            out["clock_ghz"] = res["GRBM_GUI_ACTIVE"] / 8 / out["kernel_ns_profiled"]
     if "TCC_HIT_sum" in res and "TCC_MISS_sum" in res:
         out["l2_hit_rate"] = res["TCC_HIT_sum"] / max(res["TCC_HIT_sum"] + res["TCC_MISS_sum"], 1.0)
     if "SQ_THREAD_CYCLES_VALU" in res and "SQ_ACTIVE_INST_VALU" in res:

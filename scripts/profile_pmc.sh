@@ -9,7 +9,9 @@ OUTD="$GRAFT_REPO_ROOT/${PMC_OUT:-gpurun_out}"
 mkdir -p "$OUTD"
 run() {
   local name=$1; shift
-  timeout -k 10 300 rocprofv3 --pmc "$@" --output-format csv -d "$OUTD/pmc_$name" -o run \
+  local kt=""
+  [ "$name" = clock ] && kt="--kernel-trace"  # kernel durations for the clock (GRBM_GUI_ACTIVE / 8 / ns)
+  timeout -k 10 300 rocprofv3 $kt --pmc "$@" --output-format csv -d "$OUTD/pmc_$name" -o run \
     -- python3 "$GRAFT_REPO_ROOT/bench.py" $ARGS > "$OUTD/pmc_$name.log" 2>&1
 }
 run fetch FETCH_SIZE && \

@@ -1,7 +1,9 @@
-"""Predicts strong-scaling efficiency on one GPU: renders the slab that rank 0
-of N would own (rt2_shard {tile_rows, 0, N}) and compares its kernel time with
-1/N of the whole image.  (The 8-GPU run itself is the driver's; this shows
-whether a 1/N slab still fills the chip.)"""
+"""Predicts strong-scaling efficiency on one GPU: renders the slab that every
+rank r of N would own (rt2_shard {tile_rows, r, N}) and compares the SLOWEST
+rank's time with 1/N of the whole image (a job of N ranks ends with its
+slowest slab; VERDICT r4: timing rank 0 alone under-reported it).  (The 8-GPU
+run itself is the driver's; this shows whether a 1/N slab still fills the
+chip.)"""
 import argparse
 import json
 import os
@@ -33,13 +35,14 @@ if a.cost_order >= 0:
 first = {}  # slab image of the first variant, per N: every variant must match it bit for bit
 
 
-def slab_time(sh):
+def slab_time_r(sh):
+    first_key = (sh.nranks, sh.rank)
     rows = rt2.shard_rows(spec.height, sh)
     acc = torch.zeros((rows, spec.width, 4), device="cuda")
     scene.render(u, 0, spec.frames, sh, acc.data_ptr())
     torch.cuda.synchronize()
-    ref = first.setdefault(sh.nranks, acc.clone())
-    assert torch.equal(acc, ref), f"slab 1/{sh.nranks} differs from the first variant's"
+    ref = first.setdefault(first_key, acc.clone())
+    assert torch.equal(acc, ref), f"slab {sh.rank}/{sh.nranks} differs from the first variant's"
     ts = []
     for _ in range(a.reps):
         acc.zero_()
@@ -53,9 +56,15 @@ def slab_time(sh):
 
 for var in [int(v) for v in a.variants.split(",")]:
     scene.set_variant(var)
-    out = {n: slab_time(rt2.shard(a.tile_rows, 0, n)) for n in [int(x) for x in a.ns.split(",")]}
-    base = out.get(1)
+    per = {}
+    for n in [int(x) for x in a.ns.split(",")]:
+        per[n] = [slab_time_r(rt2.shard(a.tile_rows, r, n)) for r in range(n)]
+        print(json.dumps({"progress": f"variant {var} N={n}", "slab_ms": [round(t * 1e3, 2) for t in per[n]]}),
+              file=sys.stderr, flush=True)
+    base = max(per[1]) if 1 in per else None
     print(json.dumps({"config": a.config, "traversal": a.traversal, "tile_rows": a.tile_rows, "variant": var, "cost_order": a.cost_order,
                       "name": rt2.lib().rt2_variant_name(var).decode() if var else "auto",
-                      "slab_ms": {n: round(t * 1e3, 2) for n, t in out.items()},
-                      "predicted_efficiency": {n: round(base / n / t, 3) for n, t in out.items()} if base else None}), flush=True)
+                      "slab_ms_max": {n: round(max(t) * 1e3, 2) for n, t in per.items()},
+                      "slab_ms_all": {n: [round(x * 1e3, 2) for x in t] for n, t in per.items()},
+                      "predicted_efficiency": {n: round(base / n / max(t), 3) for n, t in per.items()} if base else None}),
+          flush=True)

@@ -131,7 +131,7 @@ std::vector<Result> run(int proto, int n, const std::string& site, int fault_ran
                 rc = GATHER_SLABS(
                     t, [&](std::string&) { return 0; }, [&] { return t.issue_gather(); },
                     [&](std::string&) { return 0; }, err);
-                if (rc == 0 && t.wait_gather() != 0) rc = -2;  // the caller's own wait, under its deadline
+                if (rc == 0 && t.wait_gather() != 0) rc = -2;  // the caller waits with rt2_comm_wait (its deadline)
             } else {
                 rc = rt2p::render_gather(
                     t, true, "", r == 0, [&](bool, std::string&) { return 0; }, [&](bool) { return t.issue_gather(); },

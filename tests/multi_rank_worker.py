@@ -54,7 +54,7 @@ def main():
     rt2.resolve_rgba32f(acc.data_ptr(), rows * W, 1, slab.data_ptr(), stream)
     image = torch.zeros((H, W, 4), device="cuda") if rank == 0 else None
     comm.gather_slabs(slab.data_ptr(), W, H, sh, 0, image.data_ptr() if rank == 0 else 0, stream)
-    torch.cuda.synchronize()
+    comm.wait(stream)  # rt2_comm_wait: the gather drained under the deadline
     comm.check()
     if rank == 0:
         res["gather_slabs"] = bool(np.array_equal(image.cpu().numpy(), scene.render_host(u, 0, 1)))

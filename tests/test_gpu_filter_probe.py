@@ -189,7 +189,7 @@ def near_threshold_scene(rt2mod):
     return sd
 
 
-@pytest.mark.parametrize("variant", [150, 152, 200, 206, 227, 228, 231, 233, 212, 213, 214, 215, 216, 217, 260, 261, 262, 263, 269, 270, 237, 238, 243, 245, 247, 248, 249, 250, 252])
+@pytest.mark.parametrize("variant", [227, 228, 231, 233, 212, 213, 217, 260, 261, 262, 263, 243, 250, 252, 280, 281, 282, 283])
 def test_near_threshold_scene_bit_exact(rt2mod, oraclemod, torch_cuda, variant):
     if not rt2mod.has_variant(variant):
         pytest.skip(f"variant {variant} not in this build")

@@ -19,11 +19,11 @@ MFMA = 227
 # free-running waves and the assist kernel with the matrix filter (138, 139:
 # forced here, so every segment with helpers is a job of group-range units)
 def _mfma_variants():
-    """Every matrix-filter variant the loaded library carries (ids 130-259),
-    except the timing-only speed-of-light probes."""
+    """Every matrix-filter variant the loaded library carries (ids 130-399:
+    the product defaults 262 / 263 / 280 included)."""
     import rt2
     out = []
-    for v in range(130, 260):
+    for v in range(130, 400):
         name = rt2.lib().rt2_variant_name(v)
         if name and name.decode().startswith(("mfma", "massist")):
             out.append(v)
@@ -46,8 +46,14 @@ def torch_cuda():
     return torch
 
 
+RES_MAX_TRIS = 38 * 32  # render_mfma_k5r ("mfmar"): records resident in LDS, scenes of <= 38 groups
+
+
 def mfma_scene(rt2mod, sd=None, variant=MFMA, **kw):
     require_variant(rt2mod, variant)
+    n = sd.num_triangles if sd is not None else len(kw["triangles"])
+    if rt2mod.lib().rt2_variant_name(variant).decode().startswith("mfmar/") and n > RES_MAX_TRIS:
+        pytest.skip(f"variant {variant} holds scenes of <= {RES_MAX_TRIS} triangles")
     scene = rt2mod.Scene(sd, 0) if sd is not None else rt2mod.Scene(**kw)
     scene.set_variant(variant)
     return scene

@@ -139,9 +139,9 @@ def test_comm_gather_slabs_one_rank(rt2mod, config_scene, torch_cuda):
     slab = render_slab(rt2mod, torch, scene, u, 1, rt2mod.shard())
     image = torch.zeros_like(slab)
     comm = rt2mod.Comm(rt2mod.Comm.unique_id(), 1, 0, 0)
-    comm.gather_slabs(slab.data_ptr(), W, H, rt2mod.shard(), 0, image.data_ptr(),
-                      torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream().cuda_stream
+    comm.gather_slabs(slab.data_ptr(), W, H, rt2mod.shard(), 0, image.data_ptr(), stream)
+    comm.wait(stream)  # rt2_comm_wait: the gather drained under the RT2_COMM_TIMEOUT_S deadline
     comm.check()
     assert torch.equal(image, slab)
     comm.close()
@@ -180,6 +180,26 @@ def test_comm_one_rank_injected_faults(rt2mod, config_scene, torch_cuda, site, m
         comm.check()
         img = scene.render_host_gather(u, 0, 1, rt2mod.shard(), comm, 0)
         assert np.array_equal(img, scene.render_host(u, 0, 1))
+    comm.close()
+
+
+def test_comm_render_longer_than_timeout(rt2mod, config_scene, torch_cuda, monkeypatch):
+    """the watchdog of rt2_render_host_gather starts after the rank's
+    own render (a local render has no peer to wait for), and the render's time
+    is slack on the deadlines after it: a healthy render many times longer
+    than RT2_COMM_TIMEOUT_S completes, bit-identical to rt2_render_host."""
+    import time
+    sd, spec = config_scene("B")
+    u = rt2mod.offline_uniforms(1920, 1080, spec.bounces, 64, sd.num_triangles)
+    scene = rt2mod.Scene(sd, 0)
+    ref = scene.render_host(u, 0, 1)
+    comm = rt2mod.Comm(rt2mod.Comm.unique_id(), 1, 0, 0)
+    monkeypatch.setenv("RT2_COMM_TIMEOUT_S", "0.02")
+    t0 = time.time()
+    img = scene.render_host_gather(u, 0, 1, rt2mod.shard(), comm, 0)
+    assert time.time() - t0 > 3 * 0.02  # the render alone outlasts the deadline several times
+    assert np.array_equal(img, ref)
+    comm.check()
     comm.close()
 
 
