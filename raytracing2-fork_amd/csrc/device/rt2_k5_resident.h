@@ -31,28 +31,6 @@
 
 namespace {
 
-// The MFMA A-operand fragments of both 32-ray blocks from each lane's own 16
-// k-slots s[0..15] (lane l = ray l): block R's lane l holds ray 32R + (l & 31),
-// k-slots 8 (l >> 5) .. +7 — what the fragment rows' ds_read_b128 gave.
-// v_permlane32_swap(x, y) swaps x's lanes 32..63 with y's lanes 0..31, so with
-// x = slots 0..7 and y = slots 8..15: x becomes block 0's fragment (lanes
-// 0..31 their own slots 0..7, lanes 32..63 the slots 8..15 of rays 0..31) and
-// y block 1's.
-__device__ __forceinline__ void frag_pair(const _Float16* s, h8 out[2]) {
-    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-    const u4 lo = __builtin_bit_cast(u4, h8{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7]});
-    const u4 hi = __builtin_bit_cast(u4, h8{s[8], s[9], s[10], s[11], s[12], s[13], s[14], s[15]});
-    u4 r0, r1;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const auto r = __builtin_amdgcn_permlane32_swap(lo[k], hi[k], false, false);
-        r0[k] = r[0];
-        r1[k] = r[1];
-    }
-    out[0] = __builtin_bit_cast(h8, r0);
-    out[1] = __builtin_bit_cast(h8, r1);
-}
-
 // LDS of the resident records: NG groups x the 4 operands x 64 lanes x 16 B
 template <int NG>
 struct K5Resident {
@@ -64,7 +42,10 @@ struct K5Resident {
 // filter's range.
 template <MfmaSpec S>
 __device__ __forceinline__ bool sweep_k5_res(const RenderParams& p, const h8* rec, const f3& o, const f3& d,
-                                             float& best, int& bi, float& bestK, MfmaDiag& dg, bool upper) {
+                                             float& best, int& bi, float& bestK, MfmaDiag& dg, bool upper, int G0 = 0,
+                                             int G1 = -1) {
+    // [G0, G1): the 32-triangle groups to sweep (all by default; a range when
+    // the groups of one wave's segment are split into tail-job units)
     static_assert(S.k5 && S.no_tn && S.cthr && S.ymma && S.imax && S.minred && S.ylds == 0, "the cthr 4-product form");
     const int lane = (int)lane_id();
     const f3 m = cross(d, o);
@@ -89,18 +70,25 @@ __device__ __forceinline__ bool sweep_k5_res(const RenderParams& p, const h8* re
         frag_pair(s, y1);
     };
     build_y(bestK);
-    const int ng = (p.n_tris + 31) >> 5;
-    const h8* tb = rec + lane;
+    const int ng = G1 < 0 ? (p.n_tris + 31) >> 5 : G1, n_tris = p.n_tris;
+    cfloat* const tri = (cfloat*)p.tri;  // held across the sweep (not re-read from the kernel arguments per hot group)
+    const h8* tb = rec + (size_t)G0 * (4 * 64) + lane;
     h8 nb[4];
     auto fetch = [&]() {
+        if constexpr (S.t1_first) {
+            // T1 first: the threshold product TT, which every other product
+            // takes as its accumulator, waits for this read alone
+            nb[3] = tb[192];
+            __builtin_amdgcn_sched_barrier(0);
+        }
         nb[0] = tb[0];
         nb[1] = tb[64];
         nb[2] = tb[128];
-        nb[3] = tb[192];
+        if constexpr (!S.t1_first) nb[3] = tb[192];
         tb += 4 * 64;
     };
     if constexpr (S.prefetch) fetch();
-    for (int G = 0; G < ng; G++) {
+    for (int G = G0; G < ng; G++) {
         if constexpr (!S.prefetch) fetch();
         const h8 b0 = nb[0], b2 = nb[1], b4 = nb[2], b6 = nb[3];
         if constexpr (S.prefetch)
@@ -116,9 +104,9 @@ __device__ __forceinline__ bool sweep_k5_res(const RenderParams& p, const h8* re
                 const int tt = __builtin_ctz(m32);
                 m32 &= m32 - 1;
                 const int idx = 32 * G + tt;
-                if (idx >= p.n_tris) break;
+                if (idx >= n_tris) break;
                 if constexpr (S.diag) dg.exact += 1;
-                cfloat* tp = (cfloat*)p.tri + 12 * idx;
+                cfloat* tp = tri + 12 * idx;
                 const MtQ qq = mt_quantities(o, d, ldc4(tp), ldc4(tp + 4), ldc4(tp + 8));
                 if (mt_pass3(qq, bestK)) mt_exact(qq, idx, best, bi, bestK);
             }
@@ -126,6 +114,84 @@ __device__ __forceinline__ bool sweep_k5_res(const RenderParams& p, const h8* re
         }
     }
     return true;
+}
+
+// ---------------------------------------------------------------------------
+// Tail jobs (MfmaSpec::tail_jobs): once the item pool is dry, a wave whose
+// lanes are all done does not leave; it helps the waves of its workgroup that
+// still trace.  A pixel-frame's rays share one RNG stream, so a launch ends
+// with whole items whose segments run one after another on one lane; at the
+// end a lone wave sweeps all groups for its last few rays while the other
+// waves of its CU idle (the last ~13 % of a config B launch, more
+// of a 1/N rank slab).  A wave with <= 32 live rays (after compaction) posts
+// its segment as a JOB in the LDS left beside the records: its rays, a 64-bit
+// key per ray, and a ticket; the groups are cut into units, which the owner
+// and the helpers claim by compare-and-swap on the ticket and sweep for the
+// job's rays from scratch (bound = none), folding each ray's result into its
+// key with an LDS atomic minimum on (dst bits << 32 | triangle index).  A hit
+// has dst > 1e-6 > 0, and positive binary32 values order like their bit
+// patterns, so the minimum key is the lexicographic (dst, index) minimum: the
+// smallest distance and, among exact ties, the lowest index — what the
+// sequential strict `dst < best` scan keeps.  Each unit's sweep starts from
+// no bound, for which the filter is still conservative (it only rejects what
+// the exact test rejects); the exact test is the reference arithmetic.  So
+// the result is bit-identical to the one-wave sweep (and to the oracle).
+// Termination: an owner serves its own job's units until none is left
+// unclaimed, then waits for the claimed ones, each of which its claimer
+// finishes without waiting on anything; helpers leave when no wave of the
+// workgroup traces any more (busy == 0), which a wave signals only after its
+// last job has completed.
+constexpr int kTailSlots = 6;  // jobs at once per workgroup (the LDS beside config B's 152 KiB of records)
+struct TailBoard {
+    float4 ray[kTailSlots][32][2];            // o (xyz), d (xyz) of the job's 32 rays (lanes 0..31 after compaction)
+    unsigned long long key[kTailSlots][32];   // (dst bits << 32 | index) minimum over the units; ~0 = no hit
+    uint32_t ticket[kTailSlots];              // epoch:24 | units:4 | next unit:4
+    uint32_t done[kTailSlots];                // units finished
+    uint32_t owner[kTailSlots];               // 0 = free, wave + 1
+    uint32_t busy;                            // waves of the workgroup that may still post jobs
+};
+__device__ __forceinline__ uint32_t lds_load_acq(uint32_t* a) {
+    return __hip_atomic_load(a, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Sweeps unit u of nu of job j for the job's rays (lanes 0..31; lanes 32..63
+// carry ray 0, as a compacted owner's do) and folds the results into the keys.
+template <MfmaSpec S>
+__device__ __attribute__((noinline)) void serve_unit(const RenderParams& p, const h8* rec, TailBoard& tb, int j, int u, int nu,
+                                           MfmaDiag& dg) {
+    const int lane = (int)lane_id(), src = lane < 32 ? lane : 0;
+    const float4 ro = tb.ray[j][src][0], rdv = tb.ray[j][src][1];
+    const f3 o = mk(ro.x, ro.y, ro.z), d = mk(rdv.x, rdv.y, rdv.z);
+    const int ng = (p.n_tris + 31) >> 5;
+    const int G0 = u * ng / nu, G1 = (u + 1) * ng / nu;
+    float best = 1e38f, bestK = 1e38f * 1.0009765625f;
+    int bi = -1;
+    (void)sweep_k5_res<S>(p, rec, o, d, best, bi, bestK, dg, false, G0, G1);  // in range: the owner checked these rays
+    if (lane < 32 && bi >= 0)
+        atomicMin(&tb.key[j][lane], (unsigned long long)__float_as_uint(best) << 32 | (uint32_t)bi);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_fetch_add(&tb.done[j], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// One claim on job j: the unit index (and the job's unit count), or -1 when
+// every unit is claimed.  Lane 0 runs the compare-and-swap; the outcome is
+// broadcast to the whole wave (wave-uniform control flow).
+__device__ __forceinline__ int claim_unit(TailBoard& tb, int j, int& nu) {
+    uint32_t got = 0xffffffffu;
+    if (lane_id() == 0) {
+        uint32_t t = lds_load_acq(&tb.ticket[j]);
+        while ((t & 15u) < ((t >> 4) & 15u)) {
+            if (__hip_atomic_compare_exchange_strong(&tb.ticket[j], &t, t + 1u, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                got = t;
+                break;
+            }
+        }
+    }
+    got = (uint32_t)__builtin_amdgcn_readfirstlane((int)got);
+    if (got == 0xffffffffu) return -1;
+    nu = (int)((got >> 4) & 15u);
+    return (int)(got & 15u);
 }
 
 // render_mfma's segment loop (free-running waves: no barrier after the
@@ -136,6 +202,17 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
     static_assert(S.res_groups > 0 && !S.lockstep, "records resident in LDS; free-running waves");
     constexpr int NW = S.block / 64;
     __shared__ K5Resident<S.res_groups> rs;
+    [[maybe_unused]] TailBoard* tbp = nullptr;
+    if constexpr (S.tail_jobs > 0) {
+        __shared__ TailBoard board;
+        tbp = &board;
+        if (threadIdx.x < kTailSlots) {
+            board.ticket[threadIdx.x] = 0u;
+            board.done[threadIdx.x] = 0u;
+            board.owner[threadIdx.x] = 0u;
+        }
+        if (threadIdx.x == 0) board.busy = NW;
+    }
     {
         // every group's 4 operands by LDS-DMA (1-KiB pieces, coalesced 16 B
         // per lane, no VGPRs), dealt round-robin over the waves; then one
@@ -156,11 +233,41 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
     Lane L;
     lane_init(L);
     MfmaDiag dg;
+    [[maybe_unused]] int slot = -1;          // tail jobs: this wave's job slot once it has one
+    [[maybe_unused]] uint32_t epoch = 0;
+    const int wave = (int)(threadIdx.x >> 6);
     for (;;) {
         const RenderParams& p = kargs<RenderParams>();
         advance(L, p);
         unsigned long long act = __ballot(L.st == ST_TRACE);
-        if (!act) break;
+        if (!act) {
+            if constexpr (S.tail_jobs > 0) {
+                // every lane is done and the pool is dry: help the waves that
+                // still trace, until none does
+                TailBoard& tb = *tbp;
+                if (lane_id() == 0) {
+                    if (slot >= 0) __hip_atomic_store(&tb.owner[slot], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_fetch_add(&tb.busy, 0xffffffffu, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+                for (;;) {
+                    bool served = false;
+                    for (int j = 0; j < kTailSlots; j++) {
+                        int nu = 0;
+                        const int u = claim_unit(tb, j, nu);
+                        if (u >= 0) {
+                            serve_unit<S>(p, rs.rec, tb, j, u, nu, dg);
+                            served = true;
+                        }
+                    }
+                    if (!served) {
+                        const uint32_t b = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_load_acq(&tb.busy));
+                        if (b == 0) break;
+                        __builtin_amdgcn_s_sleep(2);
+                    }
+                }
+            }
+            break;
+        }
         if (__popcll(act) <= (unsigned)S.tail_lanes && __any(L.st == ST_DONE)) {
             float mybest = 1e38f;
             int mybi = -1;
@@ -202,8 +309,66 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
         const f3 ro = L.o, rd = L.d;
         float best = 1e38f, bestK = 1e38f * 1.0009765625f;
         int bi = -1;
+        bool swept = false;
+        if constexpr (S.tail_jobs > 0) {
+            // the pool is dry, <= 32 live rays (lanes 0..31), the rays in the
+            // filter's range, and the workgroup has waves that only help: the
+            // segment becomes a job of nu units
+            TailBoard& tb = *tbp;
+            const uint32_t helpers = NW - (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_load_acq(&tb.busy));
+            if (!upper && helpers > 0 && __any(L.st == ST_DONE) &&
+                !__ballot(!(abs_max3(ro) <= 0x1p20f && abs_max3(rd) <= 1.0001f))) {
+                if (slot < 0) {
+                    int got = -1;
+                    if (lane_id() == 0)
+                        for (int j = 0; j < kTailSlots && got < 0; j++) {
+                            uint32_t z = 0u;
+                            if (__hip_atomic_compare_exchange_strong(&tb.owner[j], &z, (uint32_t)wave + 1u,
+                                                                     __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
+                                                                     __HIP_MEMORY_SCOPE_WORKGROUP))
+                                got = j;
+                        }
+                    slot = __builtin_amdgcn_readfirstlane(got);
+                    if (slot >= 0) epoch = lds_load_acq(&tb.ticket[slot]) >> 8;
+                }
+                if (slot >= 0) {
+                    const int j = slot;
+                    const int nu = (int)min((uint32_t)S.tail_jobs, helpers + 1u);
+                    if (lane_id() < 32) {
+                        tb.ray[j][lane_id()][0] = make_float4(ro.x, ro.y, ro.z, 0.0f);
+                        tb.ray[j][lane_id()][1] = make_float4(rd.x, rd.y, rd.z, 0.0f);
+                        tb.key[j][lane_id()] = ~0ull;
+                    }
+                    epoch = (epoch + 1u) & 0xffffffu;
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    if (lane_id() == 0) {
+                        __hip_atomic_store(&tb.done[j], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_store(&tb.ticket[j], epoch << 8 | (uint32_t)nu << 4, __ATOMIC_RELEASE,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                    for (;;) {  // the owner serves its own job's units
+                        int nu2 = 0;
+                        const int u = claim_unit(tb, j, nu2);
+                        if (u < 0) break;
+                        serve_unit<S>(p, rs.rec, tb, j, u, nu2, dg);
+                    }
+                    // the units other waves claimed: each finishes without waiting
+                    while ((uint32_t)__builtin_amdgcn_readfirstlane((int)lds_load_acq(&tb.done[j])) < (uint32_t)nu)
+                        __builtin_amdgcn_s_sleep(1);
+                    if (lane_id() < 32) {
+                        const unsigned long long k = tb.key[j][lane_id()];
+                        if (k != ~0ull) {
+                            best = __uint_as_float((uint32_t)(k >> 32));
+                            bi = (int)(uint32_t)k;
+                        }
+                    }
+                    swept = true;
+                }
+            }
+        }
         // a ray outside the filter's range (wave-uniform): the drain's code
-        if (!sweep_k5_res<S>(p, rs.rec, ro, rd, best, bi, bestK, dg, upper)) coop_each(act, ro, rd, p, best, bi);
+        if (!swept && !sweep_k5_res<S>(p, rs.rec, ro, rd, best, bi, bestK, dg, upper))
+            coop_each(act, ro, rd, p, best, bi);
         if (mine) {
             L.bounce += 1;
             L.segs += 1;

@@ -34,11 +34,17 @@ namespace {
 // LDS of one workgroup's record tiles: 2 buffers x K groups x the 4 operands
 // the 5-product form reads (U0, V0, X0, T1: k16 ops 0, 2, 4, 6) as 64 lanes x
 // 16 B, the per-triangle scale tau and the m.z residual bound.
-template <int K, int NB = 2>
+template <int K, int NB = 2, bool SCALES = true>
 struct K5Tiles {
     h8 rec[NB][K * 4 * 64];
     float tau[NB][K * 32];
     float2 bnd[NB][K * 32];
+};
+// MfmaSpec::cthr: the -tn record carries the threshold, the tiles hold the
+// records alone
+template <int K, int NB>
+struct K5Tiles<K, NB, false> {
+    h8 rec[NB][K * 4 * 64];
 };
 
 __device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -60,7 +66,8 @@ __device__ __forceinline__ void wait_vm(int n) {
 // calls it in every segment the workgroup runs.  Returns false when the wave's
 // rays are outside the filter's range (nothing computed; wave-uniform).
 template <MfmaSpec S, class SH>
-__device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, SH& sh, K5Tiles<S.tile_groups, S.tile_bufs>& tl,
+__device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, SH& sh,
+                                               K5Tiles<S.tile_groups, S.tile_bufs, !S.cthr>& tl,
                                                const f3& o, const f3& d, float& best, int& bi, float& bestK,
                                                MfmaDiag& dg, bool sweeping, bool upper) {
     static_assert(S.k5 && S.ymma && S.imax && S.minred && S.tile_groups > 0, "the 5-product form");
@@ -78,18 +85,38 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, SH& sh, K5
     auto write_y = [&](float bkv) {
         _Float16 s[16];
         mfma_y_chunk(s, d, o, bkv, sc.sigma, sc.Bmax);
-        h8* row = reinterpret_cast<h8*>(&sh.ray[lane][YO]);
-        row[0] = h8{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7]};
-        row[1] = h8{s[8], s[9], s[10], s[11], s[12], s[13], s[14], s[15]};
+        if constexpr (S.perm_frag) {
+            frag_pair(s, y1);  // in registers: no rows, no wave barrier
+        } else {
+            h8* row = reinterpret_cast<h8*>(&sh.ray[lane][YO]);
+            row[0] = h8{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7]};
+            row[1] = h8{s[8], s[9], s[10], s[11], s[12], s[13], s[14], s[15]};
+        }
     };
     auto read_y = [&]() {
+        if constexpr (!S.perm_frag) {
 #pragma unroll
-        for (int R = 0; R < 2; R++) y1[R] = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][YO + 8 * hl]);
+            for (int R = 0; R < 2; R++) y1[R] = *reinterpret_cast<const h8*>(&sh.ray[32 * R + r32][YO + 8 * hl]);
+        }
     };
     if (sweeping) {
         const f3 m = cross(d, o);
         in_range = mfma_scale<S>(p.mfma_A, o, d, m, sc);
-        if (in_range) {
+        if (in_range && S.perm_frag) {
+            // MfmaSpec::perm_frag: the fragments built in registers by
+            // v_permlane32_swap (rt2_k5_resident.h frag_pair), no LDS rows
+            _Float16 s[18];
+            mfma_main_half_slots(s, d, m, sc.sigma);
+            frag_pair(s, a0);
+            const float vz = m.z * sc.sigma;
+            const _Float16 hz = (_Float16)vz;
+            const _Float16 lz = (_Float16)(vz - (float)hz);
+            zhi = wave_max_s<S>(fabsf((float)hz));
+            zlo = wave_max_s<S>(fabsf((float)lz));
+            if constexpr (S.cthr) thr = mfma_thr_bits(sc.Tw, zlo, zhi);
+            write_y(bestK);
+            compute = true;
+        } else if (in_range) {
             if constexpr (S.rows80)
                 mfma_main_row_half(&sh.ray[lane][0], d, m, sc.sigma);
             else
@@ -131,6 +158,8 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, SH& sh, K5
                 __builtin_amdgcn_global_load_lds(
                     (const __attribute__((address_space(1))) void*)(gsrc + ((size_t)(g0 + gi) * kK16Ops + op) * 64 + lane),
                     (__attribute__((address_space(3))) void*)&tl.rec[b][pc * 64], 16, 0, 0);
+            } else if constexpr (S.cthr) {
+                // (no bound or scale pieces)
             } else if (pc < nrec + nbnd) {
                 const int q = pc - nrec;
                 if (64 * q + lane < gn * 16)
@@ -248,14 +277,18 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, SH& sh, K5
                     if (mt_pass3(qq, bestK)) mt_exact(qq, idx, best, bi, bestK);
                 }
                 if (__ballot(bestK != bk0)) {
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();  // every lane has read the rows' previous Y slots
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    write_y(bestK);
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    read_y();
+                    if constexpr (S.perm_frag) {
+                        write_y(bestK);
+                    } else {
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                        __builtin_amdgcn_wave_barrier();  // every lane has read the rows' previous Y slots
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                        write_y(bestK);
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                        read_y();
+                    }
                 }
             }
         }
@@ -274,14 +307,17 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, SH& sh, K5
 template <MfmaSpec S>
 __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves))) void render_mfma_k5t(RenderParams p_arg) {
     static_assert((S.lane_lds == 2 || (S.lane_lds == 0 && S.rows80)) && S.lockstep, "lockstep segments");
+    static_assert(!S.perm_frag || S.lane_lds == 0, "register fragments: the path state stays in registers too");
     constexpr int NW = S.block / 64;
     constexpr bool stash = S.lane_lds == 2;  // the path state waits in LDS across the tile loop
     using WL = std::conditional_t<S.rows80, std::conditional_t<stash, MfmaK5nLds, MfmaK5rLds>, MfmaK16PackedLds>;
-    __shared__ WL wl[NW];
-    __shared__ K5Tiles<S.tile_groups, S.tile_bufs> tl;
+    // MfmaSpec::perm_frag: no fragment rows (one row array serves as a dummy
+    // the sweep never touches)
+    __shared__ WL wl[S.perm_frag ? 1 : NW];
+    __shared__ K5Tiles<S.tile_groups, S.tile_bufs, !S.cthr> tl;
     __shared__ BlockVote<NW> vote;
     uint32_t vote_parity = 0;
-    WL& sh = wl[threadIdx.x >> 6];
+    WL& sh = wl[S.perm_frag ? 0 : threadIdx.x >> 6];
     Lane L;
     lane_init(L);
     MfmaDiag dg;

@@ -80,6 +80,9 @@ struct MfmaSpec {
     bool cthr = false;      // k5 no_tn: the threshold rides in the products' accumulator operand (one matrix
                             // product per group, mfma_thr_frag), and the reduction is a sign-bit AND / OR
                             // (2 v_bitop3_b32 per pair instead of 2.5 min / max)
+    bool perm_frag = false; // render_mfma_k5t: fragments built in registers by v_permlane32_swap (no LDS rows)
+    int tail_jobs = 0;      // render_mfma_k5r: up to this many units per tail job (0 = no tail jobs)
+    bool t1_first = false;  // render_mfma_k5r: a group's -tn record (the threshold product's operand) is read first
     int res_groups = 0;     // render_mfma_k5r (rt2_k5_resident.h): every group's records resident in the
                             // workgroup's LDS for the whole launch (scenes of <= res_groups 32-triangle groups)
     int sol = 0;            // speed-of-light probes (WRONG images; diag clocks only): 1 = every group reads group
@@ -688,8 +691,33 @@ __device__ __forceinline__ ThrBits mfma_thr_bits(float Tw, float zlo, float zhi)
 __device__ __forceinline__ h8 mfma_thr_frag(ThrBits tb) {
     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
     const bool up = lane_id() >= 32;  // slots 8..15 of the K-half: 29, 30, 31 are elements 5, 6, 7
-    const u4 v = {0u, 0u, up ? opaque(tb.w2) : 0u, up ? opaque(tb.w3) : 0u};
+    // opaque() outside the selects: an asm value inside a ?: compiled to two
+    // exec-masked branches per group instead of two v_cndmask
+    const uint32_t w2 = opaque(tb.w2), w3 = opaque(tb.w3);
+    const u4 v = {0u, 0u, up ? w2 : 0u, up ? w3 : 0u};
     return __builtin_bit_cast(h8, v);
+}
+
+// MfmaSpec::perm_frag / render_mfma_k5r: the MFMA A-operand fragments of both 32-ray blocks from each lane's own 16
+// k-slots s[0..15] (lane l = ray l): block R's lane l holds ray 32R + (l & 31),
+// k-slots 8 (l >> 5) .. +7 — what the fragment rows' ds_read_b128 gave.
+// v_permlane32_swap(x, y) swaps x's lanes 32..63 with y's lanes 0..31, so with
+// x = slots 0..7 and y = slots 8..15: x becomes block 0's fragment (lanes
+// 0..31 their own slots 0..7, lanes 32..63 the slots 8..15 of rays 0..31) and
+// y block 1's.
+__device__ __forceinline__ void frag_pair(const _Float16* s, h8 out[2]) {
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    const u4 lo = __builtin_bit_cast(u4, h8{s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7]});
+    const u4 hi = __builtin_bit_cast(u4, h8{s[8], s[9], s[10], s[11], s[12], s[13], s[14], s[15]});
+    u4 r0, r1;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const auto r = __builtin_amdgcn_permlane32_swap(lo[k], hi[k], false, false);
+        r0[k] = r[0];
+        r1[k] = r[1];
+    }
+    out[0] = __builtin_bit_cast(h8, r0);
+    out[1] = __builtin_bit_cast(h8, r1);
 }
 
 // The five terms of 32 rays (fragments a0/a1 = the main fragment's two

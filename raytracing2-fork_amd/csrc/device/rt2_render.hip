@@ -614,14 +614,17 @@ constexpr MfmaSpec k5_tiles_spec(int K, bool no_tn, int tail, bool diag = false)
 // records resident in LDS (rt2_k5_resident.h): one workgroup per CU (3 or 4
 // waves per SIMD), scenes of <= kResGroups 32-triangle groups
 constexpr int kResGroups = 38;  // 152 KiB of k5 records (4 KiB per group) of the CU's 160 KiB
-constexpr MfmaSpec k5_res_spec(int waves, bool prefetch, bool diag = false) {
+constexpr MfmaSpec k5_res_spec(int waves, bool prefetch, bool diag = false, int tail = 4, bool t1_first = false,
+                               int jobs = 0) {
     MfmaSpec x = kMfmaK5NoTn;
     x.block = 256 * waves;
     x.waves = waves;
-    x.tail_lanes = 4;
+    x.tail_lanes = tail;
     x.lane_lds = 0;
     x.cthr = true;
     x.lockstep = false;
+    x.t1_first = t1_first;
+    x.tail_jobs = jobs;
     x.prefetch = prefetch;
     x.res_groups = kResGroups;
     x.diag = diag;
@@ -700,6 +703,18 @@ const Variant kVariants[] = {
     RT2_VARIANT(281, K_MFMA, render_mfma_k5r<k5_res_spec(3, true)>, 768, "mfmar/768/k5/notn/res38/coop4/w3/cmp/cthr/pf"),
     RT2_VARIANT(282, K_MFMA, render_mfma_k5r<k5_res_spec(4, false)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr"),
     RT2_VARIANT(283, K_MFMA, render_mfma_k5r<k5_res_spec(4, true)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/pf"),
+    RT2_VARIANT(284, K_MFMA, render_mfma_k5r<k5_res_spec(4, false, false, 4, true)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/t1f"),
+    RT2_VARIANT(285, K_MFMA, render_mfma_k5r<k5_res_spec(4, false, false, 8)>, 1024, "mfmar/1024/k5/notn/res38/coop8/w4/cmp/cthr"),
+    RT2_VARIANT(286, K_MFMA, render_mfma_k5r<k5_res_spec(4, false, false, 0)>, 1024, "mfmar/1024/k5/notn/res38/coop0/w4/cmp/cthr"),
+    RT2_VARIANT(288, K_MFMA, render_mfma_k5r<k5_res_spec(4, false, false, 4, false, 8)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/jobs8"),
+    RT2_VARIANT(289, K_MFMA, render_mfma_k5r<k5_res_spec(4, false, false, 0, false, 8)>, 1024, "mfmar/1024/k5/notn/res38/coop0/w4/cmp/cthr/jobs8"),
+    RT2_VARIANT(290, K_MFMA, render_mfma_k5r<k5_res_spec(4, false, false, 4, false, 4)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/jobs4"),
+    // the tiled kernel with register fragments (no LDS rows: bigger tiles) at 4 or 3 waves per SIMD
+    RT2_VARIANT(291, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(16, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; x.perm_frag = true; x.block = 1024; x.waves = 4; return x; }()>, 1024, "mfmat5/1024/k5/notn/tile16/coop0/w4/cmp/regs/cthr/perm"),
+    RT2_VARIANT(292, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(19, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; x.perm_frag = true; x.block = 1024; x.waves = 4; return x; }()>, 1024, "mfmat5/1024/k5/notn/tile19/coop0/w4/cmp/regs/cthr/perm"),
+    RT2_VARIANT(293, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(19, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; x.perm_frag = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile19/coop0/w3/cmp/regs/cthr/perm"),
+    RT2_VARIANT(294, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, false); x.dpp = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/dpp"),
+    RT2_VARIANT(287, K_MFMA, render_mfma_k5r<k5_res_spec(4, false, true)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/diag"),
 #ifdef RT2_EXPERIMENTS
     // earlier choices of rounds 3-4 (the 5-product form before and after the threshold moved into the accumulator,
     // the first tile forms), kept for A/B; rounds 2-3's 16x16x32 and k16 kernels are in git history
@@ -756,6 +771,8 @@ constexpr int kMfmaSlabMaxTris = 8192;
 constexpr int kMfmaSmall = 263;    // <= kMfmaSlabMaxTris triangles: k5 without -tn, 4 waves (packed path state),
                                    // cooperative drain at <= 4 live rays (config B 187.9 vs 192.9 ms for 233's 8), the
                                    // threshold in the accumulator (DESIGN.md "The threshold in the accumulator")
+constexpr int kMfmaRes = 282;      // <= kResGroups groups (config B): every record resident in LDS, 4 waves per SIMD
+                                   // (rt2_k5_resident.h): config B 164.6 vs 189.7 ms for 263, identical image
 constexpr int kMfmaSmallW3 = 262;  // ... 3 waves, when the packed fields cannot hold the launch
 constexpr int kMfmaTiles = 217;    // larger scenes: the 5-product form without -tn with workgroup-shared LDS record
                                    // tiles of 10 groups, the path state in registers (rt2_k5_tiles.h; DESIGN.md "LDS
@@ -1034,7 +1051,9 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
             // workgroup per CU), without the -tn term (config C 26.94 vs
             // 29.19 s with it; config E sample 1.56 vs 1.60 s); its path state
             // stays in registers, so it has no packed-field limits
-            if (s->n_tris <= kMfmaSlabMaxTris)
+            if (res_fits && find_variant(kMfmaRes))
+                vi = kMfmaRes;
+            else if (s->n_tris <= kMfmaSlabMaxTris)
                 vi = packed && find_variant(kMfmaSmall) ? kMfmaSmall : kMfmaSmallW3;
             else if (find_variant(kMfmaTiles))
                 vi = kMfmaTiles;

@@ -76,6 +76,7 @@ def test_comm_argument_validation(rt2mod):
     assert L.rt2_comm_init(None, 1, 0, 0, C.byref(p)) < 0
     assert L.rt2_comm_wrap(None, 0, C.byref(p)) < 0
     assert L.rt2_comm_check(None) < 0
+    assert L.rt2_comm_wait(None, None) < 0
     assert L.rt2_gather_slabs(None, None, 8, 8, rt2mod.shard(), 0, None, None) < 0
     # max_rows smaller than the largest slab of the layout
     assert L.rt2_unshard_slabs(C.c_void_p(16), 1, 8, 8, rt2mod.shard(1, 0, 2), C.c_void_p(16), None) < 0
