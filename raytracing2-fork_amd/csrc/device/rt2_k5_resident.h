@@ -157,8 +157,8 @@ __device__ __forceinline__ uint32_t lds_load_acq(uint32_t* a) {
 // Sweeps unit u of nu of job j for the job's rays (lanes 0..31; lanes 32..63
 // carry ray 0, as a compacted owner's do) and folds the results into the keys.
 template <MfmaSpec S>
-__device__ __attribute__((noinline)) void serve_unit(const RenderParams& p, const h8* rec, TailBoard& tb, int j, int u, int nu,
-                                           MfmaDiag& dg) {
+__device__ __forceinline__ void serve_unit_body(const RenderParams& p, const h8* rec, TailBoard& tb, int j, int u, int nu,
+                                                MfmaDiag& dg) {
     const int lane = (int)lane_id(), src = lane < 32 ? lane : 0;
     const float4 ro = tb.ray[j][src][0], rdv = tb.ray[j][src][1];
     const f3 o = mk(ro.x, ro.y, ro.z), d = mk(rdv.x, rdv.y, rdv.z);
@@ -171,6 +171,20 @@ __device__ __attribute__((noinline)) void serve_unit(const RenderParams& p, cons
         atomicMin(&tb.key[j][lane], (unsigned long long)__float_as_uint(best) << 32 | (uint32_t)bi);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (lane == 0) __hip_atomic_fetch_add(&tb.done[j], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+template <MfmaSpec S>
+__device__ __attribute__((noinline)) void serve_unit_call(const RenderParams& p, const h8* rec, TailBoard& tb, int j, int u,
+                                                         int nu, MfmaDiag& dg) {
+    serve_unit_body<S>(p, rec, tb, j, u, nu, dg);
+}
+// MfmaSpec::jobs_dbg: 2 = the unit inlined at its call sites (no call)
+template <MfmaSpec S>
+__device__ __forceinline__ void serve_unit(const RenderParams& p, const h8* rec, TailBoard& tb, int j, int u, int nu,
+                                           MfmaDiag& dg) {
+    if constexpr (S.jobs_dbg == 2)
+        serve_unit_body<S>(p, rec, tb, j, u, nu, dg);
+    else
+        serve_unit_call<S>(p, rec, tb, j, u, nu, dg);
 }
 
 // One claim on job j: the unit index (and the job's unit count), or -1 when
@@ -251,7 +265,7 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
                 }
                 for (;;) {
                     bool served = false;
-                    for (int j = 0; j < kTailSlots; j++) {
+                    for (int j = 0; j < (S.jobs_dbg == 1 ? 0 : kTailSlots); j++) {  // jobs_dbg 1: helpers only wait
                         int nu = 0;
                         const int u = claim_unit(tb, j, nu);
                         if (u >= 0) {
@@ -333,7 +347,8 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
                 }
                 if (slot >= 0) {
                     const int j = slot;
-                    const int nu = (int)min((uint32_t)S.tail_jobs, helpers + 1u);
+                    // jobs_dbg 4: the owner only waits, the helpers serve every unit
+                    const int nu = (int)min((uint32_t)S.tail_jobs, S.jobs_dbg == 4 ? helpers : helpers + 1u);
                     if (lane_id() < 32) {
                         tb.ray[j][lane_id()][0] = make_float4(ro.x, ro.y, ro.z, 0.0f);
                         tb.ray[j][lane_id()][1] = make_float4(rd.x, rd.y, rd.z, 0.0f);
@@ -346,11 +361,13 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
                         __hip_atomic_store(&tb.ticket[j], epoch << 8 | (uint32_t)nu << 4, __ATOMIC_RELEASE,
                                            __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
-                    for (;;) {  // the owner serves its own job's units
-                        int nu2 = 0;
-                        const int u = claim_unit(tb, j, nu2);
-                        if (u < 0) break;
-                        serve_unit<S>(p, rs.rec, tb, j, u, nu2, dg);
+                    if constexpr (S.jobs_dbg != 4) {
+                        for (;;) {  // the owner serves its own job's units
+                            int nu2 = 0;
+                            const int u = claim_unit(tb, j, nu2);
+                            if (u < 0) break;
+                            serve_unit<S>(p, rs.rec, tb, j, u, nu2, dg);
+                        }
                     }
                     // the units other waves claimed: each finishes without waiting
                     while ((uint32_t)__builtin_amdgcn_readfirstlane((int)lds_load_acq(&tb.done[j])) < (uint32_t)nu)
@@ -363,6 +380,31 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
                         }
                     }
                     swept = true;
+                    if constexpr (S.jobs_dbg == 3 || S.jobs_dbg == 5) {
+                        // debugging: the one-wave sweep beside the job's keys; mismatches counted in the
+                        // diagnostic counters (the first one described), the sweep's result shaded
+                        float b2 = 1e38f, k2 = 1e38f * 1.0009765625f;
+                        int i2 = -1;
+                        (void)sweep_k5_res<S>(p, rs.rec, ro, rd, b2, i2, k2, dg, upper);
+                        const bool bad = mine && (i2 != bi || __float_as_uint(b2) != __float_as_uint(best));
+                        if (bad) {
+                            atomicAdd(p.seg_counter + 15, 1ull);
+                            if (atomicCAS(p.seg_counter + 16, 0ull, 1ull) == 0ull) {
+                                p.seg_counter[17] = lane_id() | (unsigned long long)nu << 8 |
+                                                    (unsigned long long)__popcll(act) << 16 |
+                                                    (unsigned long long)helpers << 24;
+                                p.seg_counter[18] = (unsigned long long)(uint32_t)bi;
+                                p.seg_counter[19] = __float_as_uint(best);
+                                p.seg_counter[20] = (unsigned long long)(uint32_t)i2;
+                                p.seg_counter[21] = __float_as_uint(b2);
+                                p.seg_counter[22] = tb.key[j][lane_id() & 31];
+                            }
+                        }
+                        if constexpr (S.jobs_dbg == 3) {
+                            best = b2;
+                            bi = i2;
+                        }
+                    }
                 }
             }
         }

@@ -81,7 +81,8 @@ struct MfmaSpec {
                             // product per group, mfma_thr_frag), and the reduction is a sign-bit AND / OR
                             // (2 v_bitop3_b32 per pair instead of 2.5 min / max)
     bool perm_frag = false; // render_mfma_k5t: fragments built in registers by v_permlane32_swap (no LDS rows)
-    int tail_jobs = 0;      // render_mfma_k5r: up to this many units per tail job (0 = no tail jobs)
+    int tail_jobs = 0;
+    int jobs_dbg = 0;       // tail jobs, debugging: 1 = helpers serve no unit (owners serve all), 2 = no call      // render_mfma_k5r: up to this many units per tail job (0 = no tail jobs)
     bool t1_first = false;  // render_mfma_k5r: a group's -tn record (the threshold product's operand) is read first
     int res_groups = 0;     // render_mfma_k5r (rt2_k5_resident.h): every group's records resident in the
                             // workgroup's LDS for the whole launch (scenes of <= res_groups 32-triangle groups)

@@ -714,6 +714,13 @@ const Variant kVariants[] = {
     RT2_VARIANT(292, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(19, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; x.perm_frag = true; x.block = 1024; x.waves = 4; return x; }()>, 1024, "mfmat5/1024/k5/notn/tile19/coop0/w4/cmp/regs/cthr/perm"),
     RT2_VARIANT(293, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(19, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; x.perm_frag = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile19/coop0/w3/cmp/regs/cthr/perm"),
     RT2_VARIANT(294, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, false); x.dpp = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/dpp"),
+    RT2_VARIANT(295, K_MFMA, render_mfma_k5r<k5_res_spec(4, false, false, 4, false, 1)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/jobs1"),
+    RT2_VARIANT(296, K_MFMA, render_mfma_k5r<k5_res_spec(4, false, false, 4, false, 2)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/jobs2"),
+    RT2_VARIANT(297, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, false, false, 4, false, 8); x.jobs_dbg = 1; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/jobs8/dbg1"),
+    RT2_VARIANT(298, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, false, false, 4, false, 8); x.jobs_dbg = 2; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/jobs8/dbg2"),
+    RT2_VARIANT(299, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, false, false, 4, false, 8); x.jobs_dbg = 3; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/jobs8/dbg3"),
+    RT2_VARIANT(300, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, false, false, 4, false, 8); x.jobs_dbg = 4; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/jobs8/dbg4"),
+    RT2_VARIANT(301, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, false, false, 4, false, 8); x.jobs_dbg = 5; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/jobs8/dbg5"),
     RT2_VARIANT(287, K_MFMA, render_mfma_k5r<k5_res_spec(4, false, true)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/diag"),
 #ifdef RT2_EXPERIMENTS
     // earlier choices of rounds 3-4 (the 5-product form before and after the threshold moved into the accumulator,
@@ -774,8 +781,10 @@ constexpr int kMfmaSmall = 263;    // <= kMfmaSlabMaxTris triangles: k5 without 
 constexpr int kMfmaRes = 282;      // <= kResGroups groups (config B): every record resident in LDS, 4 waves per SIMD
                                    // (rt2_k5_resident.h): config B 164.6 vs 189.7 ms for 263, identical image
 constexpr int kMfmaSmallW3 = 262;  // ... 3 waves, when the packed fields cannot hold the launch
-constexpr int kMfmaTiles = 217;    // larger scenes: the 5-product form without -tn with workgroup-shared LDS record
-                                   // tiles of 10 groups, the path state in registers (rt2_k5_tiles.h; DESIGN.md "LDS
+constexpr int kMfmaTiles = 293;    // larger scenes (round 5): 217's LDS tiles with the fragments built in registers
+                                   // (v_permlane32_swap, no LDS rows), so the tiles grow to 19 groups: config C
+                                   // 23.63 vs 23.87 s, config E 6.14 vs 6.23 s (same images); round 4's 217:
+                                   // the 5-product form without -tn with workgroup-shared LDS record tiles of 10 groups, the path state in registers (rt2_k5_tiles.h; DESIGN.md "LDS
                                    // record tiles": config C 25.94 vs 26.66 s for 252's 4-group tiles and 32.5 s for
                                    // round 3's 227), the threshold in the accumulator (C sample 1.07 vs 1.24 s for 213)
 constexpr int kMfma = 227;  // mfma/.../k5/...: the matrix-core filter on v_mfma_f32_32x32x16_f16, 5 products per
