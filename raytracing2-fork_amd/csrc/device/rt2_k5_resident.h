@@ -89,11 +89,17 @@ __device__ __forceinline__ bool sweep_k5_res(const RenderParams& p, const h8* re
     };
     if constexpr (S.prefetch) fetch();
     for (int G = G0; G < ng; G++) {
-        if constexpr (!S.prefetch) fetch();
-        const h8 b0 = nb[0], b2 = nb[1], b4 = nb[2], b6 = nb[3];
-        if constexpr (S.prefetch)
-            if (G + 1 < ng) fetch();
-        const unsigned long long M = k5_cthr_group<S>(thr, a0, y1, b0, b2, b4, b6, upper, 0);
+        unsigned long long M;
+        if constexpr (S.rec_reread) {
+            M = k5_res_group<S>(thr, a0, y1, tb, upper);
+            tb += 4 * 64;
+        } else {
+            if constexpr (!S.prefetch) fetch();
+            const h8 b0 = nb[0], b2 = nb[1], b4 = nb[2], b6 = nb[3];
+            if constexpr (S.prefetch)
+                if (G + 1 < ng) fetch();
+            M = k5_cthr_group<S>(thr, a0, y1, b0, b2, b4, b6, upper, 0);
+        }
         if constexpr (S.diag) dg.groups += 1;
         if (M) {
             if constexpr (S.diag) dg.hot += 1;
@@ -125,9 +131,10 @@ __device__ __forceinline__ bool sweep_k5_res(const RenderParams& p, const h8* re
 // waves of its CU idle (the last ~13 % of a config B launch, more
 // of a 1/N rank slab).  A wave with <= 32 live rays (after compaction) posts
 // its segment as a JOB in the LDS left beside the records: its rays, a 64-bit
-// key per ray, and a ticket; the groups are cut into units, which the owner
-// and the helpers claim by compare-and-swap on the ticket and sweep for the
-// job's rays from scratch (bound = none), folding each ray's result into its
+// key per ray, and a ticket; the groups are cut into one unit per helper
+// (at most tail_jobs), which the helpers claim by compare-and-swap on the
+// ticket and sweep for the job's rays from scratch (bound = none), folding
+// each ray's result into its
 // key with an LDS atomic minimum on (dst bits << 32 | triangle index).  A hit
 // has dst > 1e-6 > 0, and positive binary32 values order like their bit
 // patterns, so the minimum key is the lexicographic (dst, index) minimum: the
@@ -136,11 +143,15 @@ __device__ __forceinline__ bool sweep_k5_res(const RenderParams& p, const h8* re
 // no bound, for which the filter is still conservative (it only rejects what
 // the exact test rejects); the exact test is the reference arithmetic.  So
 // the result is bit-identical to the one-wave sweep (and to the oracle).
-// Termination: an owner serves its own job's units until none is left
-// unclaimed, then waits for the claimed ones, each of which its claimer
-// finishes without waiting on anything; helpers leave when no wave of the
-// workgroup traces any more (busy == 0), which a wave signals only after its
-// last job has completed.
+// Termination: an owner posts only when helpers exist, and a helper leaves
+// only when no wave of the workgroup traces any more (busy == 0), which a wave
+// signals after its last job has completed; a claimed unit finishes without
+// waiting on anything, so the owner's wait for its units ends.  The owner
+// itself serves no unit: a form in which it served its own units (a call
+// inside its segment loop) returned correct keys but a corrupted image unless
+// further code followed the call — a code-generation effect around the call
+// that we did not isolate ("Tail jobs"); owners that only wait are
+// bit-exact.
 constexpr int kTailSlots = 6;  // jobs at once per workgroup (the LDS beside config B's 152 KiB of records)
 struct TailBoard {
     float4 ray[kTailSlots][32][2];            // o (xyz), d (xyz) of the job's 32 rays (lanes 0..31 after compaction)
@@ -157,8 +168,8 @@ __device__ __forceinline__ uint32_t lds_load_acq(uint32_t* a) {
 // Sweeps unit u of nu of job j for the job's rays (lanes 0..31; lanes 32..63
 // carry ray 0, as a compacted owner's do) and folds the results into the keys.
 template <MfmaSpec S>
-__device__ __forceinline__ void serve_unit_body(const RenderParams& p, const h8* rec, TailBoard& tb, int j, int u, int nu,
-                                                MfmaDiag& dg) {
+__device__ __attribute__((noinline)) void serve_unit(const RenderParams& p, const h8* rec, TailBoard& tb, int j, int u,
+                                                    int nu, MfmaDiag& dg) {
     const int lane = (int)lane_id(), src = lane < 32 ? lane : 0;
     const float4 ro = tb.ray[j][src][0], rdv = tb.ray[j][src][1];
     const f3 o = mk(ro.x, ro.y, ro.z), d = mk(rdv.x, rdv.y, rdv.z);
@@ -172,21 +183,6 @@ __device__ __forceinline__ void serve_unit_body(const RenderParams& p, const h8*
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (lane == 0) __hip_atomic_fetch_add(&tb.done[j], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-template <MfmaSpec S>
-__device__ __attribute__((noinline)) void serve_unit_call(const RenderParams& p, const h8* rec, TailBoard& tb, int j, int u,
-                                                         int nu, MfmaDiag& dg) {
-    serve_unit_body<S>(p, rec, tb, j, u, nu, dg);
-}
-// MfmaSpec::jobs_dbg: 2 = the unit inlined at its call sites (no call)
-template <MfmaSpec S>
-__device__ __forceinline__ void serve_unit(const RenderParams& p, const h8* rec, TailBoard& tb, int j, int u, int nu,
-                                           MfmaDiag& dg) {
-    if constexpr (S.jobs_dbg == 2)
-        serve_unit_body<S>(p, rec, tb, j, u, nu, dg);
-    else
-        serve_unit_call<S>(p, rec, tb, j, u, nu, dg);
-}
-
 // One claim on job j: the unit index (and the job's unit count), or -1 when
 // every unit is claimed.  Lane 0 runs the compare-and-swap; the outcome is
 // broadcast to the whole wave (wave-uniform control flow).
@@ -217,6 +213,13 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
     constexpr int NW = S.block / 64;
     __shared__ K5Resident<S.res_groups> rs;
     [[maybe_unused]] TailBoard* tbp = nullptr;
+    typedef uint32_t Stash[2][NW][64];
+    [[maybe_unused]] Stash* stp = nullptr;
+    if constexpr (S.pack_state) {
+        static_assert(S.tail_jobs == 0, "the stash takes the LDS the tail jobs would use");
+        __shared__ Stash stash;
+        stp = &stash;
+    }
     if constexpr (S.tail_jobs > 0) {
         __shared__ TailBoard board;
         tbp = &board;
@@ -247,6 +250,7 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
     Lane L;
     lane_init(L);
     MfmaDiag dg;
+    [[maybe_unused]] unsigned long long wsegs = 0;  // pack_state: this wave's segments
     [[maybe_unused]] int slot = -1;          // tail jobs: this wave's job slot once it has one
     [[maybe_unused]] uint32_t epoch = 0;
     const int wave = (int)(threadIdx.x >> 6);
@@ -265,7 +269,7 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
                 }
                 for (;;) {
                     bool served = false;
-                    for (int j = 0; j < (S.jobs_dbg == 1 ? 0 : kTailSlots); j++) {  // jobs_dbg 1: helpers only wait
+                    for (int j = 0; j < kTailSlots; j++) {
                         int nu = 0;
                         const int u = claim_unit(tb, j, nu);
                         if (u >= 0) {
@@ -286,9 +290,10 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
             float mybest = 1e38f;
             int mybi = -1;
             coop_each(act, L.o, L.d, p, mybest, mybi);
+            if constexpr (S.pack_state) wsegs += __popcll(__ballot(L.st == ST_TRACE));
             if (L.st == ST_TRACE) {
                 L.bounce += 1;
-                L.segs += 1;
+                if constexpr (!S.pack_state) L.segs += 1;
                 shade(L, p, mybest, mybi);
             }
             continue;
@@ -324,6 +329,18 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
         float best = 1e38f, bestK = 1e38f * 1.0009765625f;
         int bi = -1;
         bool swept = false;
+        // MfmaSpec::pack_state: across the sweep the path state's small fields
+        // wait packed in two registers (st:3 | inside:1 | bounce:12 | ray:16,
+        // x:16 | y:16: the launcher takes this form only when they fit) and
+        // item / seed in the LDS beside the records, the segment count kept
+        // per wave (a scalar) — fewer live VGPRs for the 4-wave budget
+        [[maybe_unused]] uint32_t pk0 = 0, pk1 = 0;
+        if constexpr (S.pack_state) {
+            pk0 = opaque_v((uint32_t)L.st | (uint32_t)L.inside << 3 | (uint32_t)L.bounce << 4 | (uint32_t)L.ray << 16);
+            pk1 = opaque_v((uint32_t)L.x | (uint32_t)L.y << 16);
+            (*stp)[0][wave][lane_id()] = L.item;
+            (*stp)[1][wave][lane_id()] = L.seed;
+        }
         if constexpr (S.tail_jobs > 0) {
             // the pool is dry, <= 32 live rays (lanes 0..31), the rays in the
             // filter's range, and the workgroup has waves that only help: the
@@ -347,8 +364,7 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
                 }
                 if (slot >= 0) {
                     const int j = slot;
-                    // jobs_dbg 4: the owner only waits, the helpers serve every unit
-                    const int nu = (int)min((uint32_t)S.tail_jobs, S.jobs_dbg == 4 ? helpers : helpers + 1u);
+                    const int nu = (int)min((uint32_t)S.tail_jobs, helpers);
                     if (lane_id() < 32) {
                         tb.ray[j][lane_id()][0] = make_float4(ro.x, ro.y, ro.z, 0.0f);
                         tb.ray[j][lane_id()][1] = make_float4(rd.x, rd.y, rd.z, 0.0f);
@@ -361,15 +377,8 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
                         __hip_atomic_store(&tb.ticket[j], epoch << 8 | (uint32_t)nu << 4, __ATOMIC_RELEASE,
                                            __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
-                    if constexpr (S.jobs_dbg != 4) {
-                        for (;;) {  // the owner serves its own job's units
-                            int nu2 = 0;
-                            const int u = claim_unit(tb, j, nu2);
-                            if (u < 0) break;
-                            serve_unit<S>(p, rs.rec, tb, j, u, nu2, dg);
-                        }
-                    }
-                    // the units other waves claimed: each finishes without waiting
+                    // the helpers serve the units; each claimed unit finishes
+                    // without waiting on anything
                     while ((uint32_t)__builtin_amdgcn_readfirstlane((int)lds_load_acq(&tb.done[j])) < (uint32_t)nu)
                         __builtin_amdgcn_s_sleep(1);
                     if (lane_id() < 32) {
@@ -380,45 +389,36 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
                         }
                     }
                     swept = true;
-                    if constexpr (S.jobs_dbg == 3 || S.jobs_dbg == 5) {
-                        // debugging: the one-wave sweep beside the job's keys; mismatches counted in the
-                        // diagnostic counters (the first one described), the sweep's result shaded
-                        float b2 = 1e38f, k2 = 1e38f * 1.0009765625f;
-                        int i2 = -1;
-                        (void)sweep_k5_res<S>(p, rs.rec, ro, rd, b2, i2, k2, dg, upper);
-                        const bool bad = mine && (i2 != bi || __float_as_uint(b2) != __float_as_uint(best));
-                        if (bad) {
-                            atomicAdd(p.seg_counter + 15, 1ull);
-                            if (atomicCAS(p.seg_counter + 16, 0ull, 1ull) == 0ull) {
-                                p.seg_counter[17] = lane_id() | (unsigned long long)nu << 8 |
-                                                    (unsigned long long)__popcll(act) << 16 |
-                                                    (unsigned long long)helpers << 24;
-                                p.seg_counter[18] = (unsigned long long)(uint32_t)bi;
-                                p.seg_counter[19] = __float_as_uint(best);
-                                p.seg_counter[20] = (unsigned long long)(uint32_t)i2;
-                                p.seg_counter[21] = __float_as_uint(b2);
-                                p.seg_counter[22] = tb.key[j][lane_id() & 31];
-                            }
-                        }
-                        if constexpr (S.jobs_dbg == 3) {
-                            best = b2;
-                            bi = i2;
-                        }
-                    }
                 }
             }
         }
         // a ray outside the filter's range (wave-uniform): the drain's code
         if (!swept && !sweep_k5_res<S>(p, rs.rec, ro, rd, best, bi, bestK, dg, upper))
             coop_each(act, ro, rd, p, best, bi);
+        if constexpr (S.pack_state) {
+            L.st = (int)(pk0 & 7u);
+            L.inside = ((pk0 >> 3) & 1u) != 0;
+            L.bounce = (int)((pk0 >> 4) & 0xfffu);
+            L.ray = (int)(pk0 >> 16);
+            L.x = (int)(pk1 & 0xffffu);
+            L.y = (int)(pk1 >> 16);
+            L.item = (*stp)[0][wave][lane_id()];
+            L.seed = (*stp)[1][wave][lane_id()];
+        }
+        if constexpr (S.pack_state) wsegs += __popcll(__ballot(mine));
         if (mine) {
             L.bounce += 1;
-            L.segs += 1;
+            if constexpr (!S.pack_state) L.segs += 1;
             shade(L, p, best, bi);
         }
     }
     const RenderParams& p = kargs<RenderParams>();
-    flush_counters(L, p);
+    if constexpr (S.pack_state) {
+        // segments counted per wave (a scalar), not per lane
+        if (lane_id() == 0) atomicAdd(p.seg_counter, wsegs);
+    } else {
+        flush_counters(L, p);
+    }
     if constexpr (S.diag)
         if (lane_id() == 0) {
             atomicAdd(p.seg_counter + 1, dg.groups);  // (wave, triangle group) sweeps

@@ -714,13 +714,12 @@ const Variant kVariants[] = {
     RT2_VARIANT(292, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(19, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; x.perm_frag = true; x.block = 1024; x.waves = 4; return x; }()>, 1024, "mfmat5/1024/k5/notn/tile19/coop0/w4/cmp/regs/cthr/perm"),
     RT2_VARIANT(293, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(19, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; x.perm_frag = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile19/coop0/w3/cmp/regs/cthr/perm"),
     RT2_VARIANT(294, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, false); x.dpp = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/dpp"),
-    RT2_VARIANT(295, K_MFMA, render_mfma_k5r<k5_res_spec(4, false, false, 4, false, 1)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/jobs1"),
-    RT2_VARIANT(296, K_MFMA, render_mfma_k5r<k5_res_spec(4, false, false, 4, false, 2)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/jobs2"),
-    RT2_VARIANT(297, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, false, false, 4, false, 8); x.jobs_dbg = 1; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/jobs8/dbg1"),
-    RT2_VARIANT(298, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, false, false, 4, false, 8); x.jobs_dbg = 2; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/jobs8/dbg2"),
-    RT2_VARIANT(299, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, false, false, 4, false, 8); x.jobs_dbg = 3; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/jobs8/dbg3"),
-    RT2_VARIANT(300, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, false, false, 4, false, 8); x.jobs_dbg = 4; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/jobs8/dbg4"),
-    RT2_VARIANT(301, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, false, false, 4, false, 8); x.jobs_dbg = 5; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/jobs8/dbg5"),
+    RT2_VARIANT(302, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, false); x.rec_reread = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/rr"),
+    RT2_VARIANT(303, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, false); x.rec_reread = true; x.dpp = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/rr/dpp"),
+    RT2_VARIANT(304, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, false); x.rec_reread = true; x.pack_state = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/rr/pk"),
+    RT2_VARIANT(305, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(19, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; x.perm_frag = true; x.rec_reread = true; x.y_early = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile19/coop0/w3/cmp/regs/cthr/perm/rr/ye"),
+    RT2_VARIANT(306, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(19, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; x.perm_frag = true; x.rec_reread = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile19/coop0/w3/cmp/regs/cthr/perm/rr"),
+    RT2_VARIANT(307, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, false); x.rec_reread = true; x.pack_state = true; x.y_early = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/rr/pk/ye"),
     RT2_VARIANT(287, K_MFMA, render_mfma_k5r<k5_res_spec(4, false, true)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/diag"),
 #ifdef RT2_EXPERIMENTS
     // earlier choices of rounds 3-4 (the 5-product form before and after the threshold moved into the accumulator,
@@ -1036,7 +1035,7 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     // the packed path state (lane_lds = 2) holds 16-bit x, y, rays per pixel and 12-bit bounce counts
     const bool packed = u->width <= 65535 && u->height <= 65535 && u->maxBounceCount <= 4095 &&
                         u->numRaysPerPixel <= 65535;
-    if (VP && !packed && std::strstr(VP->name, "llds2")) VP = nullptr;
+    if (VP && !packed && (std::strstr(VP->name, "llds2") || std::strstr(VP->name, "/pk"))) VP = nullptr;
     if (!VP && s->traversal == RT2_TRAVERSAL_BVH) VP = find_variant(kDefaultBvh);
     if (!VP) {
         int vi = s->n_tris <= kSmemMaxTris ? kDefaultBrute : kLargeScene;

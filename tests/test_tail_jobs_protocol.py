@@ -4,9 +4,9 @@ MfmaSpec::tail_jobs), simulated on the CPU.
 NW waves are generators interleaved at random, one LDS operation per step
 (every load, store, compare-and-swap, atomic add / min is its own step, as on
 the hardware).  Each wave traces a random number of segments; once it is in
-the tail it posts some segments as jobs of nu units (one per ray block of
-random per-unit candidate hits) and serves units, its own first, then waits;
-a wave with nothing left helps until no wave is busy.  Checks, over many
+the tail and helpers exist it posts some segments as jobs of nu = min(8,
+helpers) units (random per-unit candidate hits) and waits for them; a wave
+with nothing left helps (claims and serves units) until no wave is busy.  Checks, over many
 seeds and wave counts:
   - every unit of every posted job is served exactly once, and the owner
     reads its keys only after all of them (its result = the minimum over all
@@ -94,7 +94,7 @@ def wave(w, b, rnd, nw, split, served, log, jobs_done):
                     epoch = b.ticket[slot] >> 8
             if slot >= 0:
                 j = slot
-                nu = min(8, helpers + 1)
+                nu = min(8, helpers)
                 # the rays and the keys, then the ticket (release)
                 b.data_epoch[j] = -1  # writing
                 yield
@@ -113,12 +113,7 @@ def wave(w, b, rnd, nw, split, served, log, jobs_done):
                 else:
                     b.ticket[j] = epoch << 8 | nu << 4
                 yield
-                while True:
-                    c = yield from claim(b, j, split)
-                    if c is None:
-                        break
-                    yield from serve(b, j, c[0], c[1], c[2], served, log)
-                while b.done[j] < nu:
+                while b.done[j] < nu:  # the helpers serve the units
                     yield
                 want = [min([c[r] for c in cands if c[r] is not None], default=None) for r in range(4)]
                 assert b.key[j] == want, ("keys read before every unit was folded in", b.key[j], want)
