@@ -73,33 +73,10 @@ __device__ __forceinline__ bool sweep_k5_res(const RenderParams& p, const h8* re
     const int ng = G1 < 0 ? (p.n_tris + 31) >> 5 : G1, n_tris = p.n_tris;
     cfloat* const tri = (cfloat*)p.tri;  // held across the sweep (not re-read from the kernel arguments per hot group)
     const h8* tb = rec + (size_t)G0 * (4 * 64) + lane;
-    h8 nb[4];
-    auto fetch = [&]() {
-        if constexpr (S.t1_first) {
-            // T1 first: the threshold product TT, which every other product
-            // takes as its accumulator, waits for this read alone
-            nb[3] = tb[192];
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        nb[0] = tb[0];
-        nb[1] = tb[64];
-        nb[2] = tb[128];
-        if constexpr (!S.t1_first) nb[3] = tb[192];
-        tb += 4 * 64;
-    };
-    if constexpr (S.prefetch) fetch();
     for (int G = G0; G < ng; G++) {
-        unsigned long long M;
-        if constexpr (S.rec_reread) {
-            M = k5_res_group<S>(thr, a0, y1, tb, upper);
-            tb += 4 * 64;
-        } else {
-            if constexpr (!S.prefetch) fetch();
-            const h8 b0 = nb[0], b2 = nb[1], b4 = nb[2], b6 = nb[3];
-            if constexpr (S.prefetch)
-                if (G + 1 < ng) fetch();
-            M = k5_cthr_group<S>(thr, a0, y1, b0, b2, b4, b6, upper, 0);
-        }
+        const h8 b0 = tb[0], b2 = tb[64], b4 = tb[128], b6 = tb[192];
+        tb += 4 * 64;
+        const unsigned long long M = k5_cthr_group<S>(thr, a0, y1, b0, b2, b4, b6, upper, 0);
         if constexpr (S.diag) dg.groups += 1;
         if (M) {
             if constexpr (S.diag) dg.hot += 1;
@@ -213,13 +190,6 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
     constexpr int NW = S.block / 64;
     __shared__ K5Resident<S.res_groups> rs;
     [[maybe_unused]] TailBoard* tbp = nullptr;
-    typedef uint32_t Stash[2][NW][64];
-    [[maybe_unused]] Stash* stp = nullptr;
-    if constexpr (S.pack_state) {
-        static_assert(S.tail_jobs == 0, "the stash takes the LDS the tail jobs would use");
-        __shared__ Stash stash;
-        stp = &stash;
-    }
     if constexpr (S.tail_jobs > 0) {
         __shared__ TailBoard board;
         tbp = &board;
@@ -250,7 +220,6 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
     Lane L;
     lane_init(L);
     MfmaDiag dg;
-    [[maybe_unused]] unsigned long long wsegs = 0;  // pack_state: this wave's segments
     [[maybe_unused]] int slot = -1;          // tail jobs: this wave's job slot once it has one
     [[maybe_unused]] uint32_t epoch = 0;
     const int wave = (int)(threadIdx.x >> 6);
@@ -290,10 +259,9 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
             float mybest = 1e38f;
             int mybi = -1;
             coop_each(act, L.o, L.d, p, mybest, mybi);
-            if constexpr (S.pack_state) wsegs += __popcll(__ballot(L.st == ST_TRACE));
             if (L.st == ST_TRACE) {
                 L.bounce += 1;
-                if constexpr (!S.pack_state) L.segs += 1;
+                L.segs += 1;
                 shade(L, p, mybest, mybi);
             }
             continue;
@@ -329,18 +297,6 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
         float best = 1e38f, bestK = 1e38f * 1.0009765625f;
         int bi = -1;
         bool swept = false;
-        // MfmaSpec::pack_state: across the sweep the path state's small fields
-        // wait packed in two registers (st:3 | inside:1 | bounce:12 | ray:16,
-        // x:16 | y:16: the launcher takes this form only when they fit) and
-        // item / seed in the LDS beside the records, the segment count kept
-        // per wave (a scalar) — fewer live VGPRs for the 4-wave budget
-        [[maybe_unused]] uint32_t pk0 = 0, pk1 = 0;
-        if constexpr (S.pack_state) {
-            pk0 = opaque_v((uint32_t)L.st | (uint32_t)L.inside << 3 | (uint32_t)L.bounce << 4 | (uint32_t)L.ray << 16);
-            pk1 = opaque_v((uint32_t)L.x | (uint32_t)L.y << 16);
-            (*stp)[0][wave][lane_id()] = L.item;
-            (*stp)[1][wave][lane_id()] = L.seed;
-        }
         if constexpr (S.tail_jobs > 0) {
             // the pool is dry, <= 32 live rays (lanes 0..31), the rays in the
             // filter's range, and the workgroup has waves that only help: the
@@ -395,30 +351,14 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
         // a ray outside the filter's range (wave-uniform): the drain's code
         if (!swept && !sweep_k5_res<S>(p, rs.rec, ro, rd, best, bi, bestK, dg, upper))
             coop_each(act, ro, rd, p, best, bi);
-        if constexpr (S.pack_state) {
-            L.st = (int)(pk0 & 7u);
-            L.inside = ((pk0 >> 3) & 1u) != 0;
-            L.bounce = (int)((pk0 >> 4) & 0xfffu);
-            L.ray = (int)(pk0 >> 16);
-            L.x = (int)(pk1 & 0xffffu);
-            L.y = (int)(pk1 >> 16);
-            L.item = (*stp)[0][wave][lane_id()];
-            L.seed = (*stp)[1][wave][lane_id()];
-        }
-        if constexpr (S.pack_state) wsegs += __popcll(__ballot(mine));
         if (mine) {
             L.bounce += 1;
-            if constexpr (!S.pack_state) L.segs += 1;
+            L.segs += 1;
             shade(L, p, best, bi);
         }
     }
     const RenderParams& p = kargs<RenderParams>();
-    if constexpr (S.pack_state) {
-        // segments counted per wave (a scalar), not per lane
-        if (lane_id() == 0) atomicAdd(p.seg_counter, wsegs);
-    } else {
-        flush_counters(L, p);
-    }
+    flush_counters(L, p);
     if constexpr (S.diag)
         if (lane_id() == 0) {
             atomicAdd(p.seg_counter + 1, dg.groups);  // (wave, triangle group) sweeps

@@ -227,10 +227,7 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, SH& sh,
             // slots, padded by 2^-10 for its own rounding ("The
             // 5-product form")
             unsigned long long M;
-            if constexpr (S.cthr && S.rec_reread) {
-                // the operands re-read from the tile per 32-ray block (k5_res_group)
-                M = k5_res_group<S>(thr, a0, y1, &tl.rec[b][gi * 4 * 64 + lane], upper);
-            } else if constexpr (S.cthr) {
+            if constexpr (S.cthr) {
                 M = k5_cthr_group<S>(thr, a0, y1, b0, b2, b4, b6, upper, sh);
             } else {
             const float Tl = tau * sc.Tw + (bnd.x * zlo + bnd.y * zhi) * 1.0009765625f;

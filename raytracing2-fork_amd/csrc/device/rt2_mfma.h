@@ -72,8 +72,6 @@ struct MfmaSpec {
     int tile_groups = 0;    // k5 (render_mfma_k5t, rt2_k5_tiles.h): 32-triangle groups per LDS record tile
     bool dpp = false;       // the per-segment wave maxima by DPP lane moves (wave_max_dpp) instead of ds_bpermute
     bool rows80 = false;    // no_tn: 80-B fragment rows, main slots 0..15 (the first K-half) + the Y slots at 16..31
-    bool wg_pool = false;   // render_mfma_pool (rt2_k5_pool.h): the workgroup's rays packed into 32-ray blocks
-    bool wg_split = false;  // ... and with <= 2 blocks, each block's sweep split over the waves by triangle range
     int tile_bufs = 2;      // render_mfma_k5t: record tile buffers (3: tile t+2 in flight while t is swept)
     int ylds = 0;           // cthr: each block's Y fragment (1), or its main and Y fragments (2), read from LDS right
                             // before its products
@@ -82,10 +80,6 @@ struct MfmaSpec {
                             // (2 v_bitop3_b32 per pair instead of 2.5 min / max)
     bool perm_frag = false; // render_mfma_k5t: fragments built in registers by v_permlane32_swap (no LDS rows)
     int tail_jobs = 0;      // render_mfma_k5r: up to this many units per tail job (0 = no tail jobs)
-    bool pack_state = false;  // render_mfma_k5r: small path-state fields packed / in LDS across the sweep
-    bool rec_reread = false;  // render_mfma_k5r / k5t: U0, V0, X0 read from LDS per 32-ray block (fewer live VGPRs)
-    bool y_early = false;     // k5_res_group: a block's four products issued together, one reduction pass
-    bool t1_first = false;  // render_mfma_k5r: a group's -tn record (the threshold product's operand) is read first
     int res_groups = 0;     // render_mfma_k5r (rt2_k5_resident.h): every group's records resident in the
                             // workgroup's LDS for the whole launch (scenes of <= res_groups 32-triangle groups)
     int sol = 0;            // speed-of-light probes (WRONG images; diag clocks only): 1 = every group reads group
@@ -786,59 +780,6 @@ __device__ __forceinline__ unsigned long long k5_cthr_group(ThrBits tb, const h8
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < 16; i++)  // (t3 & Y) | acc: one chain, no OR tree (which costs 0.5 more per pair)
-            acc = __builtin_amdgcn_bitop3_b32(t3[i], __float_as_int(Y[i]), acc, 0xEA);
-        if (R == 1) __builtin_amdgcn_sched_barrier(0);
-    }
-    return __ballot(acc < 0);
-}
-
-// MfmaSpec::rec_reread: one group's filter (k5_cthr_group's arithmetic, term
-// for term) with the record operands read from LDS where each product needs
-// them — U0, V0, X0 once per 32-ray block — instead of held for the whole
-// group: 12 fewer VGPRs live across the reductions (the 4-wave budget's
-// spills; the LDS reads are 4 more ds_read_b128 per group and wave).  The
-// address is laundered per block so the compiler reloads instead of keeping
-// the first block's operands live.
-template <MfmaSpec S>
-__device__ __forceinline__ unsigned long long k5_res_group(ThrBits tb, const h8* a0, const h8* y1, const h8* g,
-                                                           bool upper) {
-    const f16v zero = {};
-    const h8 b6 = g[192];
-    const f16v TT = __builtin_amdgcn_mfma_f32_32x32x16_f16(mfma_thr_frag(tb), b6, zero, 0, 0, 0);
-    int acc = 0;
-#pragma unroll
-    for (int R = 0; R < 2; R++) {
-        if (R == 1 && !upper) break;
-        const h8* gr = g + (R == 0 ? 0 : (int)opaque(0u));
-        const f16v U = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[R], gr[0], TT, 0, 0, 0);
-        const f16v V = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[R], gr[64], TT, 0, 0, 0);
-        const f16v X = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[R], gr[128], TT, 0, 0, 0);
-        if constexpr (S.y_early) {
-            // MfmaSpec::y_early: all four products issued back to back, then
-            // one pass over the pairs ((U & V & X) & Y) | acc: one product
-            // latency per block instead of two (16 more VGPRs live).  (A Y
-            // product merely placed before the U V X reduction in the source
-            // is sunk below it by instruction selection.)
-            const f16v Y = __builtin_amdgcn_mfma_f32_32x32x16_f16(y1[R], b6, TT, 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int i = 0; i < 16; i++)
-                acc = __builtin_amdgcn_bitop3_b32(
-                    __builtin_amdgcn_bitop3_b32(__float_as_int(U[i]), __float_as_int(V[i]), __float_as_int(X[i]), 0x80),
-                    __float_as_int(Y[i]), acc, 0xEA);
-            if (R == 1) __builtin_amdgcn_sched_barrier(0);
-            continue;
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        int t3[16];
-#pragma unroll
-        for (int i = 0; i < 16; i++)  // U & V & X (LUT index 4 S0 + 2 S1 + S2)
-            t3[i] = __builtin_amdgcn_bitop3_b32(__float_as_int(U[i]), __float_as_int(V[i]), __float_as_int(X[i]), 0x80);
-        __builtin_amdgcn_sched_barrier(0);
-        const f16v Y = __builtin_amdgcn_mfma_f32_32x32x16_f16(y1[R], b6, TT, 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < 16; i++)  // (t3 & Y) | acc
             acc = __builtin_amdgcn_bitop3_b32(t3[i], __float_as_int(Y[i]), acc, 0xEA);
         if (R == 1) __builtin_amdgcn_sched_barrier(0);
     }

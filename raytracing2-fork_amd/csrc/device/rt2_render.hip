@@ -536,13 +536,8 @@ constexpr SmemSpec kSmemDefault{.block = 256, .group = 8, .filter = Filter::Max3
 constexpr SmemSpec kSmemMid{.block = 256, .group = 8, .filter = Filter::Max3, .tail = Tail::Coop, .tail_lanes = 32,
                             .waves = 1, .stats = false};
 constexpr SplitSpec kSplitSmall{.waves_per_ray = 4, .group = 8, .filter = Filter::Max3, .waves = 6};
-constexpr AssistSpec kAssist8{.waves_per_block = 8, .group = 8, .filter = Filter::Max3, .waves = 6, .coop_rays = 32};
 constexpr SmemSpec kSmemFree{.block = 256, .group = 8, .filter = Filter::Max3, .tail = Tail::Coop, .tail_lanes = 32,
                              .waves = 6, .stats = false, .lockstep = false};
-constexpr SmemSpec kSmemLock128{.block = 128, .group = 8, .filter = Filter::Max3, .tail = Tail::Coop, .tail_lanes = 32,
-                                .waves = 6, .stats = false, .lockstep = true};
-constexpr SmemSpec kSmemLock512{.block = 512, .group = 8, .filter = Filter::Max3, .tail = Tail::Coop, .tail_lanes = 32,
-                                .waves = 6, .stats = false, .lockstep = true};
 constexpr AssistSpec assist12_x(int coop) {
     return AssistSpec{.waves_per_block = 12, .group = 8, .filter = Filter::Max3, .waves = 6, .coop_rays = coop};
 }
@@ -614,8 +609,7 @@ constexpr MfmaSpec k5_tiles_spec(int K, bool no_tn, int tail, bool diag = false)
 // records resident in LDS (rt2_k5_resident.h): one workgroup per CU (3 or 4
 // waves per SIMD), scenes of <= kResGroups 32-triangle groups
 constexpr int kResGroups = 38;  // 152 KiB of k5 records (4 KiB per group) of the CU's 160 KiB
-constexpr MfmaSpec k5_res_spec(int waves, bool prefetch, bool diag = false, int tail = 4, bool t1_first = false,
-                               int jobs = 0) {
+constexpr MfmaSpec k5_res_spec(int waves, bool diag = false, int tail = 4, int jobs = 0) {
     MfmaSpec x = kMfmaK5NoTn;
     x.block = 256 * waves;
     x.waves = waves;
@@ -623,9 +617,7 @@ constexpr MfmaSpec k5_res_spec(int waves, bool prefetch, bool diag = false, int 
     x.lane_lds = 0;
     x.cthr = true;
     x.lockstep = false;
-    x.t1_first = t1_first;
     x.tail_jobs = jobs;
-    x.prefetch = prefetch;
     x.res_groups = kResGroups;
     x.diag = diag;
     return x;
@@ -633,41 +625,6 @@ constexpr MfmaSpec k5_res_spec(int waves, bool prefetch, bool diag = false, int 
 constexpr Bvh3Spec kBvhDefault{.block = 256, .thresh = 16, .slab = Slab::Markstein, .waves = 5, .diag = false};
 
 #ifdef RT2_EXPERIMENTS
-constexpr MfmaSpec kMfmaT8Y{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true, .ymma = true,
-                            .tshift = 12};
-constexpr MfmaSpec kMfmaT8Y4D{.block = 256, .waves = 4, .tail_lanes = 8, .imax = true, .minred = true, .diag = true,
-                              .ymma = true, .tshift = 12};
-constexpr MfmaSpec kMfmaT8{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true};
-constexpr MfmaSpec kMfmaIM{.block = 256, .waves = 2, .tail_lanes = 16, .imax = true, .minred = true};
-constexpr MfmaSpec kMfmaT4{.block = 256, .waves = 2, .tail_lanes = 4, .imax = true, .minred = true};
-constexpr MfmaSpec kMfmaT0{.block = 256, .waves = 2, .tail_lanes = 0, .imax = true, .minred = true};
-constexpr MfmaSpec kMfmaT8F{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true, .lockstep = false};
-constexpr MfmaSpec kMfmaT8D{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true, .diag = true};
-constexpr MfmaSpec kMfmaT8YD{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true, .diag = true,
-                              .ymma = true};
-constexpr MfmaSpec kMfmaT8Y3{.block = 256, .waves = 3, .tail_lanes = 8, .imax = true, .minred = true, .ymma = true};
-constexpr MfmaSpec kMfmaT8Y4T10{.block = 256, .waves = 4, .tail_lanes = 8, .imax = true, .minred = true, .ymma = true};
-constexpr MfmaSpec kMfmaT8Y4T14{.block = 256, .waves = 4, .tail_lanes = 8, .imax = true, .minred = true, .ymma = true,
-                                 .tshift = 14};
-constexpr MfmaSpec kMfmaT8YDT12{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true, .diag = true,
-                                 .ymma = true, .tshift = 12};
-constexpr MfmaSpec kMfmaT8Y2W{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true, .ymma = true,
-                               .tshift = 12, .lds_pad = 36864};  // 2 workgroups per CU: 2 waves per SIMD
-constexpr MfmaSpec kMfmaT8Y1W{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .minred = true, .ymma = true,
-                               .tshift = 12, .lds_pad = 69632};  // 1 workgroup per CU
-constexpr MfmaSpec kMfmaT8P3{.block = 256, .waves = 3, .tail_lanes = 8, .imax = true, .prefetch = true, .minred = true};
-constexpr MfmaSpec kMfmaT8P2{.block = 256, .waves = 2, .tail_lanes = 8, .imax = true, .prefetch = true, .minred = true};
-constexpr MfmaSpec kMfmaT4F{.block = 256, .waves = 2, .tail_lanes = 4, .imax = true, .minred = true, .lockstep = false};
-constexpr AssistSpec kAssistM{.waves_per_block = 12, .group = 8, .filter = Filter::Max3, .waves = 3, .coop_rays = 32,
-                              .mfma = true};
-constexpr AssistSpec kAssistMM{.waves_per_block = 12, .group = 8, .filter = Filter::Max3, .waves = 3, .coop_rays = 32,
-                               .mfma = true, .minred = true};
-constexpr MfmaSpec kMfmaI{.block = 256, .waves = 2, .tail_lanes = 16, .imax = true};
-constexpr MfmaSpec kMfmaDefault{.block = 256, .waves = 2, .tail_lanes = 16};
-constexpr MfmaSpec kMfmaIP{.block = 256, .waves = 2, .tail_lanes = 16, .imax = true, .prefetch = true};
-constexpr MfmaSpec kMfmaP{.block = 256, .waves = 2, .tail_lanes = 16, .prefetch = true};
-constexpr MfmaSpec kMfmaI4{.block = 256, .waves = 4, .tail_lanes = 16, .imax = true};
-constexpr MfmaSpec kMfmaIP4{.block = 256, .waves = 4, .tail_lanes = 16, .imax = true, .prefetch = true};
 constexpr SmemSpec smem_x(int g, Filter f, Tail t, int lanes, int w, bool stats = false) {
     return SmemSpec{.block = 256, .group = g, .filter = f, .tail = t, .tail_lanes = lanes, .waves = w, .stats = stats};
 }
@@ -699,29 +656,16 @@ const Variant kVariants[] = {
     RT2_VARIANT(217, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(10, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile10/coop0/w3/cmp/rows80/regs/cthr"),
     // scenes of <= 38 groups (1,216 triangles: config B): every group's records resident in LDS for the whole
     // launch (rt2_k5_resident.h), fragments built in registers by v_permlane32_swap, waves run free
-    RT2_VARIANT(280, K_MFMA, render_mfma_k5r<k5_res_spec(3, false)>, 768, "mfmar/768/k5/notn/res38/coop4/w3/cmp/cthr"),
-    RT2_VARIANT(281, K_MFMA, render_mfma_k5r<k5_res_spec(3, true)>, 768, "mfmar/768/k5/notn/res38/coop4/w3/cmp/cthr/pf"),
-    RT2_VARIANT(282, K_MFMA, render_mfma_k5r<k5_res_spec(4, false)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr"),
-    RT2_VARIANT(283, K_MFMA, render_mfma_k5r<k5_res_spec(4, true)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/pf"),
-    RT2_VARIANT(284, K_MFMA, render_mfma_k5r<k5_res_spec(4, false, false, 4, true)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/t1f"),
-    RT2_VARIANT(285, K_MFMA, render_mfma_k5r<k5_res_spec(4, false, false, 8)>, 1024, "mfmar/1024/k5/notn/res38/coop8/w4/cmp/cthr"),
-    RT2_VARIANT(286, K_MFMA, render_mfma_k5r<k5_res_spec(4, false, false, 0)>, 1024, "mfmar/1024/k5/notn/res38/coop0/w4/cmp/cthr"),
-    RT2_VARIANT(288, K_MFMA, render_mfma_k5r<k5_res_spec(4, false, false, 4, false, 8)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/jobs8"),
-    RT2_VARIANT(289, K_MFMA, render_mfma_k5r<k5_res_spec(4, false, false, 0, false, 8)>, 1024, "mfmar/1024/k5/notn/res38/coop0/w4/cmp/cthr/jobs8"),
-    RT2_VARIANT(290, K_MFMA, render_mfma_k5r<k5_res_spec(4, false, false, 4, false, 4)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/jobs4"),
-    // the tiled kernel with register fragments (no LDS rows: bigger tiles) at 4 or 3 waves per SIMD
-    RT2_VARIANT(291, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(16, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; x.perm_frag = true; x.block = 1024; x.waves = 4; return x; }()>, 1024, "mfmat5/1024/k5/notn/tile16/coop0/w4/cmp/regs/cthr/perm"),
-    RT2_VARIANT(292, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(19, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; x.perm_frag = true; x.block = 1024; x.waves = 4; return x; }()>, 1024, "mfmat5/1024/k5/notn/tile19/coop0/w4/cmp/regs/cthr/perm"),
+    RT2_VARIANT(282, K_MFMA, render_mfma_k5r<k5_res_spec(4)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr"),
+    // the default above 8,192 triangles (round 5): 217 with the fragments built in registers (no LDS rows), so the
+    // tiles hold 19 groups
     RT2_VARIANT(293, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(19, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; x.perm_frag = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile19/coop0/w3/cmp/regs/cthr/perm"),
-    RT2_VARIANT(294, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, false); x.dpp = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/dpp"),
-    RT2_VARIANT(302, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, false); x.rec_reread = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/rr"),
-    RT2_VARIANT(303, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, false); x.rec_reread = true; x.dpp = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/rr/dpp"),
-    RT2_VARIANT(304, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, false); x.rec_reread = true; x.pack_state = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/rr/pk"),
-    RT2_VARIANT(305, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(19, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; x.perm_frag = true; x.rec_reread = true; x.y_early = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile19/coop0/w3/cmp/regs/cthr/perm/rr/ye"),
-    RT2_VARIANT(306, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(19, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; x.perm_frag = true; x.rec_reread = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile19/coop0/w3/cmp/regs/cthr/perm/rr"),
-    RT2_VARIANT(307, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, false); x.rec_reread = true; x.pack_state = true; x.y_early = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/rr/pk/ye"),
-    RT2_VARIANT(287, K_MFMA, render_mfma_k5r<k5_res_spec(4, false, true)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/diag"),
 #ifdef RT2_EXPERIMENTS
+    // records resident in LDS at 3 waves per SIMD; tail jobs (DESIGN.md "Tail jobs", measured slower); the
+    // resident kernel's diagnostic counters
+    RT2_VARIANT(280, K_MFMA, render_mfma_k5r<k5_res_spec(3)>, 768, "mfmar/768/k5/notn/res38/coop4/w3/cmp/cthr"),
+    RT2_VARIANT(288, K_MFMA, render_mfma_k5r<k5_res_spec(4, false, 4, 8)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/jobs8"),
+    RT2_VARIANT(287, K_MFMA, render_mfma_k5r<k5_res_spec(4, true)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/diag"),
     // earlier choices of rounds 3-4 (the 5-product form before and after the threshold moved into the accumulator,
     // the first tile forms), kept for A/B; rounds 2-3's 16x16x32 and k16 kernels are in git history
     RT2_VARIANT(231, K_MFMA, render_mfma<kMfmaK5NoTn>, 256, "mfma/256/k5/notn/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"),
@@ -1035,7 +979,7 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     // the packed path state (lane_lds = 2) holds 16-bit x, y, rays per pixel and 12-bit bounce counts
     const bool packed = u->width <= 65535 && u->height <= 65535 && u->maxBounceCount <= 4095 &&
                         u->numRaysPerPixel <= 65535;
-    if (VP && !packed && (std::strstr(VP->name, "llds2") || std::strstr(VP->name, "/pk"))) VP = nullptr;
+    if (VP && !packed && std::strstr(VP->name, "llds2")) VP = nullptr;
     if (!VP && s->traversal == RT2_TRAVERSAL_BVH) VP = find_variant(kDefaultBvh);
     if (!VP) {
         int vi = s->n_tris <= kSmemMaxTris ? kDefaultBrute : kLargeScene;

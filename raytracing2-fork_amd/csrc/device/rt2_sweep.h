@@ -91,11 +91,6 @@ __device__ __forceinline__ uint32_t opaque(uint32_t x) {
     asm volatile("" : "+s"(x));
     return x;
 }
-// ... a per-lane value (VGPR): the packed form is what stays live
-__device__ __forceinline__ uint32_t opaque_v(uint32_t x) {
-    asm volatile("" : "+v"(x));
-    return x;
-}
 
 // The kernel's first argument in the kernarg segment, through a pointer the
 // compiler cannot treat as loop-invariant: its fields are loaded (s_load from

@@ -13,14 +13,15 @@ from test_gpu_parity import assert_exact, oracle_mean
 pytestmark = pytest.mark.gpu
 
 MFMA = 227
-# product kernel: render_mfma (integer max of the terms, one compare per group,
-# cooperative drain at <= 8 live rays); experiment build: f32 max, a compare
-# per pair, record prefetch, 4 waves/SIMD, other drain thresholds,
-# free-running waves and the assist kernel with the matrix filter (138, 139:
-# forced here, so every segment with helpers is a job of group-range units)
+# every matrix-filter variant of the loaded library runs each case: the
+# product build's automatic kernels (227, 262, 263, the LDS-resident 282 and
+# the LDS-tiled 217 / 293); the experiment build adds its A/B variants
+# (other drain thresholds, wave counts, record tiles, tail jobs: 288)
+
+
 def _mfma_variants():
     """Every matrix-filter variant the loaded library carries (ids 130-399:
-    the product defaults 262 / 263 / 280 included)."""
+    the product defaults 262 / 263 / 282 / 293 included)."""
     import rt2
     out = []
     for v in range(130, 400):
