@@ -223,10 +223,29 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
     [[maybe_unused]] int slot = -1;          // tail jobs: this wave's job slot once it has one
     [[maybe_unused]] uint32_t epoch = 0;
     const int wave = (int)(threadIdx.x >> 6);
+    // diag wave timeline (p.wave_log, render_mfma's 10-word layout: start,
+    // first lane out of items, end, segment rounds with two 32-ray blocks /
+    // one / - / cooperative drain, HW_ID | XCC_ID << 32, shader clocks)
+    [[maybe_unused]] unsigned long long wl_t0 = 0, wl_c0 = 0, wl_dry = 0, wl_r2 = 0, wl_r1 = 0, wl_coop = 0;
+    if constexpr (S.diag) {
+        wl_t0 = __builtin_amdgcn_s_memrealtime();
+        wl_c0 = __builtin_amdgcn_s_memtime();
+    }
     for (;;) {
         const RenderParams& p = kargs<RenderParams>();
         advance(L, p);
         unsigned long long act = __ballot(L.st == ST_TRACE);
+        if constexpr (S.diag) {
+            if (!wl_dry && __any(L.st == ST_DONE)) wl_dry = __builtin_amdgcn_s_memrealtime();
+            if (act) {
+                if (__popcll(act) <= (unsigned)S.tail_lanes && __any(L.st == ST_DONE))
+                    wl_coop++;
+                else if (__popcll(act) <= 32)
+                    wl_r1++;
+                else
+                    wl_r2++;
+            }
+        }
         if (!act) {
             if constexpr (S.tail_jobs > 0) {
                 // every lane is done and the pool is dry: help the waves that
@@ -265,6 +284,27 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
                 shade(L, p, mybest, mybi);
             }
             continue;
+        }
+        if constexpr (S.fair_prio) {
+            // MfmaSpec::fair_prio.  A SIMD's four waves start together, and
+            // in a rank slab each lane holds about one item (a pixel's 64
+            // rays, one after another): the SIMD is done when its slowest
+            // wave is.  The arbiter issues by priority, then age, so with
+            // equal priorities the oldest wave runs ahead and the youngest
+            // ends alone, latency-bound, for ~3 ms of a 25-ms 1/8 slab.  Here
+            // a wave's priority rises with the rays its slowest lane has left
+            // (quartiles of the rays per pixel): waves that fall behind take
+            // the issue slots back, and the SIMD's waves end together.
+            const float left = wave_max((float)(L.st == ST_TRACE ? p.R - L.ray : 0));
+            const int q = (int)(left * 4.0f - 1.0f) / p.R;
+            if (q >= 3)
+                __builtin_amdgcn_s_setprio(3);
+            else if (q == 2)
+                __builtin_amdgcn_s_setprio(2);
+            else if (q == 1)
+                __builtin_amdgcn_s_setprio(1);
+            else
+                __builtin_amdgcn_s_setprio(0);
         }
         bool upper = true;
         if constexpr (S.compact) {
@@ -359,6 +399,26 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
     }
     const RenderParams& p = kargs<RenderParams>();
     flush_counters(L, p);
+    if constexpr (S.diag)
+        if (p.wave_log) {
+            const uint32_t gw = blockIdx.x * NW + (uint32_t)wave;
+            const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+            const unsigned long long hw = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+                                          (unsigned long long)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32;
+            if (lane_id() == 0 && gw < p.wave_log_n) {
+                unsigned long long* e = p.wave_log + 10 * (size_t)gw;
+                e[0] = wl_t0;
+                e[1] = wl_dry;
+                e[2] = __builtin_amdgcn_s_memrealtime();
+                e[3] = wl_r2;
+                e[4] = wl_r1;
+                e[5] = 0;
+                e[6] = wl_coop;
+                e[7] = hw;
+                e[8] = wl_c0;
+                e[9] = c1;
+            }
+        }
     if constexpr (S.diag)
         if (lane_id() == 0) {
             atomicAdd(p.seg_counter + 1, dg.groups);  // (wave, triangle group) sweeps

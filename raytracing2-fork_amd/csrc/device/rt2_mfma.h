@@ -80,6 +80,8 @@ struct MfmaSpec {
                             // (2 v_bitop3_b32 per pair instead of 2.5 min / max)
     bool perm_frag = false; // render_mfma_k5t: fragments built in registers by v_permlane32_swap (no LDS rows)
     int tail_jobs = 0;      // render_mfma_k5r: up to this many units per tail job (0 = no tail jobs)
+    bool fair_prio = false;  // render_mfma_k5r: issue priority (s_setprio) by the rays the wave's slowest lane has
+                             // left, quartiles of the rays per pixel (fair share among a SIMD's waves)
     int res_groups = 0;     // render_mfma_k5r (rt2_k5_resident.h): every group's records resident in the
                             // workgroup's LDS for the whole launch (scenes of <= res_groups 32-triangle groups)
     int sol = 0;            // speed-of-light probes (WRONG images; diag clocks only): 1 = every group reads group

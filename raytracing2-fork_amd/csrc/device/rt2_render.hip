@@ -657,6 +657,9 @@ const Variant kVariants[] = {
     // scenes of <= 38 groups (1,216 triangles: config B): every group's records resident in LDS for the whole
     // launch (rt2_k5_resident.h), fragments built in registers by v_permlane32_swap, waves run free
     RT2_VARIANT(282, K_MFMA, render_mfma_k5r<k5_res_spec(4)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr"),
+    // ... with fair-share issue priority (rank slabs: < kResSlabItems items per lane; DESIGN.md "Fair-share issue
+    // priority")
+    RT2_VARIANT(298, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4); x.fair_prio = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/fair"),
     // the default above 8,192 triangles (round 5): 217 with the fragments built in registers (no LDS rows), so the
     // tiles hold 19 groups
     RT2_VARIANT(293, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(19, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; x.perm_frag = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile19/coop0/w3/cmp/regs/cthr/perm"),
@@ -666,6 +669,7 @@ const Variant kVariants[] = {
     RT2_VARIANT(280, K_MFMA, render_mfma_k5r<k5_res_spec(3)>, 768, "mfmar/768/k5/notn/res38/coop4/w3/cmp/cthr"),
     RT2_VARIANT(288, K_MFMA, render_mfma_k5r<k5_res_spec(4, false, 4, 8)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/jobs8"),
     RT2_VARIANT(287, K_MFMA, render_mfma_k5r<k5_res_spec(4, true)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/diag"),
+    RT2_VARIANT(299, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, true); x.fair_prio = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/fair/diag"),
     // earlier choices of rounds 3-4 (the 5-product form before and after the threshold moved into the accumulator,
     // the first tile forms), kept for A/B; rounds 2-3's 16x16x32 and k16 kernels are in git history
     RT2_VARIANT(231, K_MFMA, render_mfma<kMfmaK5NoTn>, 256, "mfma/256/k5/notn/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"),
@@ -723,6 +727,10 @@ constexpr int kMfmaSmall = 263;    // <= kMfmaSlabMaxTris triangles: k5 without 
                                    // threshold in the accumulator (DESIGN.md "The threshold in the accumulator")
 constexpr int kMfmaRes = 282;      // <= kResGroups groups (config B): every record resident in LDS, 4 waves per SIMD
                                    // (rt2_k5_resident.h): config B 164.6 vs 189.7 ms for 263, identical image
+constexpr int kMfmaResSlab = 298;  // ... launches with < kResSlabItems items per resident lane (rank slabs): the
+                                   // same kernel with fair-share issue priority (MfmaSpec::fair_prio): config B 1/8
+                                   // slab 23.5 vs 25.5 ms, 1/2 85.8 vs 88.7 ms; whole images unchanged or ~1 % slower
+constexpr unsigned long long kResSlabItems = 6;
 constexpr int kMfmaSmallW3 = 262;  // ... 3 waves, when the packed fields cannot hold the launch
 constexpr int kMfmaTiles = 293;    // larger scenes (round 5): 217's LDS tiles with the fragments built in registers
                                    // (v_permlane32_swap, no LDS rows), so the tiles grow to 19 groups: config C
@@ -1003,8 +1011,14 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
             // workgroup per CU), without the -tn term (config C 26.94 vs
             // 29.19 s with it; config E sample 1.56 vs 1.60 s); its path state
             // stays in registers, so it has no packed-field limits
-            if (res_fits && find_variant(kMfmaRes))
+            if (res_fits && find_variant(kMfmaRes)) {
                 vi = kMfmaRes;
+                // a SIMD's waves start together with a few items per lane:
+                // fair share, so that they also end together (DESIGN.md
+                // "Fair-share issue priority")
+                const unsigned long long lanes = (unsigned long long)s->num_cus * (unsigned long long)find_variant(kMfmaRes)->block;
+                if (p.n_items < kResSlabItems * lanes && find_variant(kMfmaResSlab)) vi = kMfmaResSlab;
+            }
             else if (s->n_tris <= kMfmaSlabMaxTris)
                 vi = packed && find_variant(kMfmaSmall) ? kMfmaSmall : kMfmaSmallW3;
             else if (find_variant(kMfmaTiles))

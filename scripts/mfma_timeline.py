@@ -21,6 +21,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="B")
 ap.add_argument("--runs", default="210:1,222:8,210:8", help="variant:N pairs (slab 1/N of the image)")
 ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out"))
+ap.add_argument("--wg-waves", type=int, default=4, help="waves per workgroup (16 for the resident kernel 287)")
 a = ap.parse_args()
 sd, spec = rt2.build_config_scene(a.config)
 u = rt2.offline_uniforms(spec.width, spec.height, spec.bounces, spec.rays, sd.num_triangles)
@@ -77,7 +78,12 @@ for run in a.runs.split(","):
     simd_work = np.bincount(inv, weights=work)
     simd_end = np.zeros(len(keys))
     np.maximum.at(simd_end, inv, end)
-    wg = idx // 4
+    wg = idx // a.wg_waves
+    # per SIMD: how long its last wave ran alone (last end - second-to-last end)
+    lone = []
+    for k in range(len(keys)):
+        e = np.sort(end[inv == k])
+        lone.append(e[-1] - e[-2] if len(e) > 1 else 0.0)
     wkeys, winv = np.unique(wg, return_inverse=True)
     wg_end = np.zeros(len(wkeys))
     np.maximum.at(wg_end, winv, end)
@@ -91,5 +97,7 @@ for run in a.runs.split(","):
         "rounds_drain_pct": pct(coop),
         "block_sweeps_total": int(work.sum()), "simd_block_sweeps_pct": pct(simd_work),
         "simd_work_max_over_mean": round(float(simd_work.max() / simd_work.mean()), 4),
+        "simd_lone_ms_pct": pct(np.array(lone)),
+        "wave_work_pct": pct(work), "wave_work_max_over_mean": round(float(work.max() / work.mean()), 4),
         "clock_ghz_pct": pct((g[:, 9] - g[:, 8]) / np.maximum(g[:, 2] - g[:, 0], 1) / 10.0),
     }), flush=True)

@@ -189,7 +189,7 @@ def near_threshold_scene(rt2mod):
     return sd
 
 
-@pytest.mark.parametrize("variant", [227, 228, 231, 233, 212, 213, 217, 260, 261, 262, 263, 243, 250, 252, 280, 282, 288, 293])
+@pytest.mark.parametrize("variant", [227, 228, 231, 233, 212, 213, 217, 260, 261, 262, 263, 243, 250, 252, 280, 282, 288, 293, 298])
 def test_near_threshold_scene_bit_exact(rt2mod, oraclemod, torch_cuda, variant):
     if not rt2mod.has_variant(variant):
         pytest.skip(f"variant {variant} not in this build")

@@ -106,7 +106,7 @@ def test_full_frame_every_pixel(rt2mod, oraclemod, config_scene, torch_cuda, cfg
     u = rt2mod.offline_uniforms(W, H, spec.bounces, spec.rays, sd.num_triangles)
     scene = rt2mod.Scene(sd, 0)
     img = scene.render_host(u, 0, 1)
-    assert _last_variant(rt2mod, scene) == (AUTO_SMALL if cfg == "B" else AUTO_TILES)
+    assert _last_variant(rt2mod, scene) == (AUTO_RES if cfg == "B" else AUTO_TILES)
     st = scene.stats(reset=True)
     assert st.samples == W * H * spec.rays
     scene.set_traversal("bvh")
@@ -129,7 +129,9 @@ def _last_variant(rt2mod, scene):
     return rt2mod.lib().rt2_variant_name(lv.value).decode()
 
 
-AUTO_TILES = "mfmat5/768/k5/notn/tile10/coop0/w3/cmp/rows80/regs/cthr"  # variant 217: > 8,192 triangles, LDS record tiles
+AUTO_TILES = "mfmat5/768/k5/notn/tile19/coop0/w3/cmp/regs/cthr/perm"  # variant 293: > 8,192 triangles, LDS record tiles
+AUTO_RES = "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr"  # 282: <= 38 groups (1,216 triangles), records resident in LDS
+AUTO_RES_SLAB = "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/fair"  # 298: the same, < 6 items per lane (rank slabs)
 AUTO_SMALL = "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp/cthr/yl1"  # 263: <= 8,192 triangles
 AUTO_SMALL_W3 = "mfma/256/k5/notn/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp/cthr"  # 262: packed fields too small
 
@@ -152,11 +154,26 @@ def test_auto_variant_large_scene(rt2mod, oraclemod, config_scene, torch_cuda):
     assert_exact(img2[::5], ref, "config C, 5000 bounces")
 
 
+def _scene_between_res_and_tiles(rt2mod, config_scene):
+    """Config B's scene plus 800 small triangles behind the camera (at z 11-14;
+    it sits at z = 10 looking down -z): 2,008
+    triangles, above the LDS-resident kernel's 38 groups and below the tiled
+    kernel's 8,192 (the L2-resident 4-wave kernel's range)."""
+    _, spec = config_scene("B")
+    sd, _ = rt2mod.build_config_scene("B")  # a fresh copy (config_scene's is shared)
+    rng = np.random.default_rng(3)
+    for i in range(800):
+        c = (float(rng.uniform(-4, 4)), 5.0 + float(rng.uniform(-4, 4)), 11.0 + float(rng.uniform(0, 3)))
+        sd.add_triangle(c, (c[0] + 0.1, c[1], c[2]), (c[0], c[1] + 0.1, c[2]), 0)
+    return sd, spec
+
+
 def test_auto_variant_packed_state_limits(rt2mod, oraclemod, config_scene, torch_cuda):
-    """Small scenes run the 4-wave build, whose path state packs the bounce
-    count into 12 bits; a bounce limit above 4095 takes the 3-wave build of
-    the same form — same image either way."""
-    sd, spec = config_scene("B")
+    """Scenes between 38 and 256 groups run the 4-wave L2-resident build, whose
+    path state packs the bounce count into 12 bits; a bounce limit above 4095
+    takes the 3-wave build of the same form — same image either way."""
+    sd, spec = _scene_between_res_and_tiles(rt2mod, config_scene)
+    assert 38 * 32 < sd.num_triangles <= 8192
     u = rt2mod.offline_uniforms(40, 24, spec.bounces, 3, sd.num_triangles)
     scene = rt2mod.Scene(sd, 0)
     img = scene.render_host(u, 0, 1)
@@ -172,16 +189,17 @@ def test_auto_variant_packed_state_limits(rt2mod, oraclemod, config_scene, torch
 
 
 def test_auto_variant_by_items_per_lane(rt2mod, config_scene, torch_cuda):
-    """The launcher picks the matrix-core filter kernel for the full config B
-    image and for its 1/2, 1/4 and 1/8 slabs (the assist
-    kernel serves slabs of scenes outside the matrix filter's range), and every
-    slab is bit-identical to the same rows of the full image."""
+    """The launcher picks the LDS-resident matrix-filter kernel for the full
+    config B image and its fair-share build for the 1/2, 1/4 and 1/8 slabs
+    (fewer than 6 items per lane; DESIGN.md "Fair-share issue priority"; the
+    assist kernel serves slabs of scenes outside the matrix filter's range),
+    and every slab is bit-identical to the same rows of the full image."""
     sd, spec = config_scene("B")
     u = rt2mod.offline_uniforms(spec.width, spec.height, spec.bounces, spec.rays, sd.num_triangles)
     scene = rt2mod.Scene(sd, 0)
     full = scene.render_host(u, 0, 1)
-    assert _last_variant(rt2mod, scene) == AUTO_SMALL
-    for n, want in ((2, AUTO_SMALL), (4, AUTO_SMALL), (8, AUTO_SMALL)):
+    assert _last_variant(rt2mod, scene) == AUTO_RES
+    for n, want in ((2, AUTO_RES_SLAB), (4, AUTO_RES_SLAB), (8, AUTO_RES_SLAB)):
         sh = rt2mod.shard(1, n - 1, n)
         img = scene.render_host(u, 0, 1, sh)
         assert _last_variant(rt2mod, scene) == want
@@ -361,11 +379,11 @@ def test_frame_split_identical(rt2mod, oraclemod, config_scene, torch_cuda, trav
 
 
 # brute-force kernel variants that change the schedule, not the arithmetic:
-# the product variants (0 = automatic, 86, 92, 227/262/263 = the matrix filter, 217 = its LDS-tiled form,
-# 136 = the scalar path forced) and, in an experiment build, the A/B
+# the product variants (0 = automatic, 86, 92, 227/262/263 = the matrix filter, 217/293 = its LDS-tiled forms,
+# 282/298 = its LDS-resident forms, 136 = the scalar path forced) and, in an experiment build, the A/B
 # variants (masked/plk filters, resident LDS, cooperative and team tail modes,
 # split waves, the round-1 slab kernels, occupancy hints)
-BRUTE_VARIANTS = [0, 86, 92, 217, 227, 262, 263, 136] + ([213, 231, 243, 252, 260, 261, 150, 152, 200, 206, 228, 233, 250, 137, 138, 139, 140, 143, 144, 145, 146] if EXPERIMENTS else []) + ([22, 24, 28, 52, 64, 65, 66, 67, 68, 70, 71, 72, 73, 74, 76, 79, 80, 84, 85, 87, 89, 95, 97, 101, 104, 106,
+BRUTE_VARIANTS = [0, 86, 92, 217, 227, 262, 263, 282, 293, 298, 136] + ([213, 231, 243, 252, 260, 261, 150, 152, 200, 206, 228, 233, 250, 137, 138, 139, 140, 143, 144, 145, 146] if EXPERIMENTS else []) + ([22, 24, 28, 52, 64, 65, 66, 67, 68, 70, 71, 72, 73, 74, 76, 79, 80, 84, 85, 87, 89, 95, 97, 101, 104, 106,
                                  90] if EXPERIMENTS else [])
 
 
