@@ -2,7 +2,7 @@
 # Round 5 measurement call (stages by environment flag; each stops the script on failure):
 #   TESTS=1     GPU suite + smoke
 #   BENCH=1     the default bench line (config B + the C / E / scalar-VALU legs, CPU baseline)
-#   STATS=1     rocprofv3 --kernel-trace --stats of a config B bench run (per-kernel averages, csv)
+#   STATS="B C" rocprofv3 --kernel-trace --stats of a bench run per config (per-kernel averages, csv)
 #   PMC_CONFIGS PMC passes (scripts/profile_pmc.sh) of the bench's render kernel per config ("B C E")
 #   SHARD="B D" every rank's slab on one GPU (scripts/shard_probe.py), automatic kernel
 # Summaries: python scripts/parse_pmc.py <config> with PMC_DIR=gpurun_out/pmc<config> (CPU side).
@@ -19,10 +19,14 @@ if [ -n "${BENCH}" ]; then
   timeout -k 10 900 python bench.py ${BENCH_ARGS} > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail -20 gpurun_out/bench.err; exit 1; }
   echo "bench ok"
 fi
-if [ -n "${STATS}" ]; then
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/stats -o run -- python3 bench.py --no-cpu-baseline --no-config-c --no-config-e --no-scalar --no-alt > gpurun_out/stats.log 2>&1 || { echo "stats failed"; tail -20 gpurun_out/stats.log; exit 1; }
-  echo "stats ok"
-fi
+for c in ${STATS}; do
+  case $c in
+    B) a="" ; d=stats ;;
+    *) a="--config $c --steps 1 --warmup 0" ; d=stats$c ;;
+  esac
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$d -o run -- python3 bench.py --no-cpu-baseline --no-config-c --no-config-e --no-scalar --no-alt $a > gpurun_out/$d.log 2>&1 || { echo "stats $c failed"; tail -20 gpurun_out/$d.log; exit 1; }
+  echo "stats $c ok"
+done
 for c in ${PMC_CONFIGS}; do
   case $c in
     B) a="" ;;
