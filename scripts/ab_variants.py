@@ -76,6 +76,7 @@ for rnd in range(a.rounds):
                            lane_survivors=c[5], frac_groups_exact=c[3] / c[2], exact_iters_per_group=c[4] / c[2],
                            lane_survivor_rate=c[5] / (c[2] * 64 * 4),
                            wave_end_spread_ms=(c[7] - c[6]) * 1e-5 if c[7] > c[6] else None)
+            diag[v]["raw"] = [int(x) for x in c[:16]]
             tt = [c[9], c[10], c[11], c[12]]  # render_mfma diag: shader clocks per phase (advance, sweep, shade, tail)
             if sum(tt):
                 diag[v]["clock_share"] = dict(zip(("advance", "sweep", "shade", "tail"),
