@@ -289,6 +289,12 @@ def attach_traffic(rf, config, variant, kern_ms):
                                     f"{digest[:12]})"}
 
 
+def progress(msg):
+    """One progress line on stderr (the JSON line alone goes to stdout): a
+    long run (config D, the C / E legs) shows that it is alive."""
+    print(f"bench.py: {msg}", file=sys.stderr, flush=True)
+
+
 def timed_renders(torch, rt2, scene, u, frames, sh, accum, image, steps, stream):
     """`steps` renders, each bracketed by HIP events on the stream it runs on;
     returns (wall seconds, mean kernel ms, stats)."""
@@ -406,6 +412,7 @@ def config_leg(torch, rt2, stream, threads, host, seconds, do_cpu, name="C"):
            "triangles": sd.num_triangles}
     legs, imgs = {}, {}
     for trav, steps, warm in (("bvh", 3, 1), ("brute", 1, 0)):
+        progress(f"config {name}: {trav} ({steps} step(s))")
         scene.set_traversal(trav)
         for _ in range(warm):
             accum.zero_()
@@ -424,6 +431,7 @@ def config_leg(torch, rt2, stream, threads, host, seconds, do_cpu, name="C"):
     nd = int((imgs["brute"][..., :3] != imgs["bvh"][..., :3]).any(-1).sum())
     out["pixels_brute_vs_bvh_differing"] = nd
     if do_cpu:
+        progress(f"config {name}: CPU baseline and parity sample")
         res, parity = cpu_baseline(sd, spec, u, imgs, threads, seconds)
         desc = (f"{res['bvh']['pixels']} of {spec.width * spec.height} pixels (BVH mode; brute mode "
                 f"{res['brute']['pixels']}), evenly spread in raster order, full {spec.rays * spec.frames} spp, "
@@ -491,10 +499,12 @@ def main():
     def step():
         return rdist.render_distributed(renderer, spec.height, spec.width, args.tile_rows, rank, world)
 
+    progress(f"config {spec.name}: {args.warmup} warmup step(s)")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     scene.stats(reset=True)
+    progress(f"config {spec.name}: {args.steps} timed step(s)")
 
     stream = torch.cuda.current_stream()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -576,6 +586,7 @@ def main():
     if world == 1 and not args.no_alt and (alt == "bvh" or sd.num_triangles <= 20000):
         # the other closest-hit algorithm on the same workload, same timing
         # bracket (reported beside the headline, never as `value`)
+        progress(f"config {spec.name}: the {alt} traversal beside the headline")
         scene.set_traversal(alt)
         scene.set_variant(0)
         renderer.accum.zero_()
@@ -607,6 +618,7 @@ def main():
         # reference's 53-FLOP Moller-Trumbore per pair on the FP32 VALU, no
         # MFMA (render_smem forced) — its VALU roofline is the physical one
         # for that kernel; same workload, same bracket, never `value`
+        progress(f"config {spec.name}: the scalar-VALU kernel (variant {SCALAR_VARIANT})")
         scene.set_variant(SCALAR_VARIANT)
         renderer.accum.zero_()
         scene.render(u, 0, spec.frames, renderer.sh, renderer.accum.data_ptr(), 0, stream.cuda_stream)
@@ -628,6 +640,7 @@ def main():
     import oracle  # test infrastructure: the CPU baseline and the parity checker only
     threads, host = oracle.default_threads(), oracle.host_cpu_info()
     if world == 1 and not args.no_cpu_baseline:
+        progress(f"config {spec.name}: CPU baseline and parity sample")
         res, parity = cpu_baseline(sd, spec, u, gpu_imgs, threads, args.cpu_seconds)
         desc = (f"{res['bvh']['pixels']} of {spec.width * spec.height} pixels (BVH mode; brute mode "
                 f"{res['brute']['pixels']}), i = floor(k*{spec.width * spec.height}/n) in raster order, full spp, "
@@ -639,6 +652,7 @@ def main():
         torch.cuda.empty_cache()
         for name, skip in (("C", args.no_config_c), ("E", args.no_config_e)):
             if not skip:
+                progress(f"config {name} leg")
                 out[f"config_{name}"] = config_leg(torch, rt2, stream, threads, host, args.cpu_seconds,
                                                    not args.no_cpu_baseline, name)
                 torch.cuda.empty_cache()
