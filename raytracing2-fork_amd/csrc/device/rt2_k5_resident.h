@@ -70,13 +70,15 @@ __device__ __forceinline__ bool sweep_k5_res(const RenderParams& p, const h8* re
         frag_pair(s, y1);
     };
     build_y(bestK);
+    // MfmaSpec::thr_hoist: the threshold fragment once per sweep
+    [[maybe_unused]] const h8 tfh = S.thr_hoist ? mfma_thr_frag(thr) : h8{};
     const int ng = G1 < 0 ? (p.n_tris + 31) >> 5 : G1, n_tris = p.n_tris;
     cfloat* const tri = (cfloat*)p.tri;  // held across the sweep (not re-read from the kernel arguments per hot group)
     const h8* tb = rec + (size_t)G0 * (4 * 64) + lane;
     for (int G = G0; G < ng; G++) {
         const h8 b0 = tb[0], b2 = tb[64], b4 = tb[128], b6 = tb[192];
         tb += 4 * 64;
-        const unsigned long long M = k5_cthr_group<S>(thr, a0, y1, b0, b2, b4, b6, upper, 0);
+        const unsigned long long M = k5_cthr_group<S>(thr, a0, y1, b0, b2, b4, b6, upper, 0, tfh);
         if constexpr (S.diag) dg.groups += 1;
         if (M) {
             if constexpr (S.diag) dg.hot += 1;

@@ -80,6 +80,7 @@ struct MfmaSpec {
                             // (2 v_bitop3_b32 per pair instead of 2.5 min / max)
     bool perm_frag = false; // render_mfma_k5t: fragments built in registers by v_permlane32_swap (no LDS rows)
     int tail_jobs = 0;      // render_mfma_k5r: up to this many units per tail job (0 = no tail jobs)
+    bool thr_hoist = false;  // k5_cthr_group: the threshold fragment built once per sweep, not once per group
     bool fair_prio = false;  // render_mfma_k5r: issue priority (s_setprio) by the rays the wave's slowest lane has
                              // left, quartiles of the rays per pixel (fair share among a SIMD's waves)
     int res_groups = 0;     // render_mfma_k5r (rt2_k5_resident.h): every group's records resident in the
@@ -749,12 +750,12 @@ __device__ __forceinline__ K16Terms k16_terms(const h8& a0, const h8& a1, const 
 template <MfmaSpec S, class SH>
 __device__ __forceinline__ unsigned long long k5_cthr_group(ThrBits tb, const h8* a0, const h8* y1, const h8& b0,
                                                             const h8& b2, const h8& b4, const h8& b6, bool upper,
-                                                            const SH& sh) {
+                                                            const SH& sh, const h8& tfh = h8{}) {
     static_assert(S.k5 && S.no_tn && S.sol == 0, "the 4-product form");
     [[maybe_unused]] constexpr int YO = S.rows80 ? 16 : 32;
     [[maybe_unused]] const int r32 = (int)lane_id() & 31, hl = (int)lane_id() >> 5;
     const f16v zero = {};
-    const f16v TT = __builtin_amdgcn_mfma_f32_32x32x16_f16(mfma_thr_frag(tb), b6, zero, 0, 0, 0);
+    const f16v TT = __builtin_amdgcn_mfma_f32_32x32x16_f16(S.thr_hoist ? tfh : mfma_thr_frag(tb), b6, zero, 0, 0, 0);
     int acc = 0;
 #pragma unroll
     for (int R = 0; R < 2; R++) {

@@ -618,6 +618,7 @@ constexpr MfmaSpec k5_res_spec(int waves, bool diag = false, int tail = 4, int j
     x.cthr = true;
     x.lockstep = false;
     x.tail_jobs = jobs;
+    x.thr_hoist = true;  // the threshold fragment once per sweep (config B 158.9 vs 160.2, 166.3 vs 167.5 ms)
     x.res_groups = kResGroups;
     x.diag = diag;
     return x;
