@@ -168,6 +168,25 @@ def _scene_between_res_and_tiles(rt2mod, config_scene):
     return sd, spec
 
 
+@pytest.mark.parametrize("extra,want", [(8, "res"), (9, "small")], ids=["1216-tris", "1217-tris"])
+def test_auto_variant_resident_boundary(rt2mod, oraclemod, torch_cuda, extra, want):
+    """The LDS-resident kernel holds scenes of at most 38 groups (1,216
+    triangles): config B's 1,208 triangles plus 8 take it, plus 9 (a 39th
+    group of one triangle) take the L2-resident 4-wave kernel — bit-exact
+    either way, the last group's padding included."""
+    sd, spec = rt2mod.build_config_scene("B")
+    for i in range(extra):  # small triangles behind the camera (z = 10, looking down -z)
+        x = -3.0 + 0.7 * i
+        sd.add_triangle((x, 4.0, 12.0), (x + 0.3, 4.0, 12.0), (x, 4.3, 12.0), 0)
+    assert sd.num_triangles == 1208 + extra
+    u = rt2mod.offline_uniforms(64, 36, spec.bounces, 4, sd.num_triangles)
+    scene = rt2mod.Scene(sd, 0)
+    img = scene.render_host(u, 0, 1)
+    assert _last_variant(rt2mod, scene) == (AUTO_RES_SLAB if want == "res" else AUTO_SMALL)
+    ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(36), 0, 1)
+    assert_exact(img, ref, f"{sd.num_triangles} triangles")
+
+
 def test_auto_variant_packed_state_limits(rt2mod, oraclemod, config_scene, torch_cuda):
     """Scenes between 38 and 256 groups run the 4-wave L2-resident build, whose
     path state packs the bounce count into 12 bits; a bounce limit above 4095
