@@ -66,6 +66,24 @@ def test_traffic_attached_only_for_the_same_kernel(profile_dir):
     assert rf["traffic"] == 99
 
 
+def test_frac_at_clock_from_the_profile(profile_dir):
+    """A matrix-bound roofline is priced at the clock its PMC pass measured
+    (VERDICT r4 item 2): peak x clock / 2.4 GHz, only for the digest-matched
+    kernel; a VALU-bound leg carries no clock figures."""
+    with open(profile_dir / "pmc_configB.json", "w") as f:
+        json.dump({"config": "B", "kernel_variant": "mfmar/x", "kernel_source_sha256": "digest-brute",
+                   "hbm_bytes_per_launch": 10, "clock_ghz": 1.92}, f)
+    rf = bench.roofline(1.0214e12, 0, 160.0, 8.4e8, 1208, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr")
+    assert rf["bound"] == "mfma"
+    bench.attach_traffic(rf, "B", "mfmar/x", 160.0)
+    assert rf["clock_ghz"] == 1.92
+    assert rf["peak_at_clock"] == pytest.approx(rf["peak"] * 1.92 / 2.4, rel=1e-3)
+    assert rf["frac_at_clock"] == pytest.approx(rf["frac"] * 2.4 / 1.92, rel=1e-3)
+    rf = bench.roofline(1e9, 0, 100.0)  # the scalar path: VALU-bound
+    bench.attach_traffic(rf, "B", "mfmar/x", 100.0)
+    assert "frac_at_clock" not in rf
+
+
 def test_roofline_figures():
     tests, kern_ms = 1.0214e12, 520.0
     rf = bench.roofline(tests, 0, kern_ms)
