@@ -619,6 +619,7 @@ constexpr MfmaSpec k5_res_spec(int waves, bool diag = false, int tail = 4, int j
     x.lockstep = false;
     x.tail_jobs = jobs;
     x.thr_hoist = true;  // the threshold fragment once per sweep (config B 158.9 vs 160.2, 166.3 vs 167.5 ms)
+    x.dpp = true;        // the segment's wave maxima by DPP lane moves (159.4 vs 160.4, 163.1 vs 164.6 ms)
     x.res_groups = kResGroups;
     x.diag = diag;
     return x;
@@ -657,20 +658,20 @@ const Variant kVariants[] = {
     RT2_VARIANT(217, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(10, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile10/coop0/w3/cmp/rows80/regs/cthr"),
     // scenes of <= 38 groups (1,216 triangles: config B): every group's records resident in LDS for the whole
     // launch (rt2_k5_resident.h), fragments built in registers by v_permlane32_swap, waves run free
-    RT2_VARIANT(282, K_MFMA, render_mfma_k5r<k5_res_spec(4)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr"),
+    RT2_VARIANT(282, K_MFMA, render_mfma_k5r<k5_res_spec(4)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/dpp"),
     // ... with fair-share issue priority (rank slabs: < kResSlabItems items per lane; DESIGN.md "Fair-share issue
     // priority")
-    RT2_VARIANT(298, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4); x.fair_prio = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/fair"),
+    RT2_VARIANT(298, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4); x.fair_prio = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/fair/dpp"),
     // the default above 8,192 triangles (round 5): 217 with the fragments built in registers (no LDS rows), so the
     // tiles hold 19 groups
     RT2_VARIANT(293, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(19, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; x.perm_frag = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile19/coop0/w3/cmp/regs/cthr/perm"),
 #ifdef RT2_EXPERIMENTS
     // records resident in LDS at 3 waves per SIMD; tail jobs (DESIGN.md "Tail jobs", measured slower); the
     // resident kernel's diagnostic counters
-    RT2_VARIANT(280, K_MFMA, render_mfma_k5r<k5_res_spec(3)>, 768, "mfmar/768/k5/notn/res38/coop4/w3/cmp/cthr"),
-    RT2_VARIANT(288, K_MFMA, render_mfma_k5r<k5_res_spec(4, false, 4, 8)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/jobs8"),
-    RT2_VARIANT(287, K_MFMA, render_mfma_k5r<k5_res_spec(4, true)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/diag"),
-    RT2_VARIANT(299, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, true); x.fair_prio = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/fair/diag"),
+    RT2_VARIANT(280, K_MFMA, render_mfma_k5r<k5_res_spec(3)>, 768, "mfmar/768/k5/notn/res38/coop4/w3/cmp/cthr/dpp"),
+    RT2_VARIANT(288, K_MFMA, render_mfma_k5r<k5_res_spec(4, false, 4, 8)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/jobs8/dpp"),
+    RT2_VARIANT(287, K_MFMA, render_mfma_k5r<k5_res_spec(4, true)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/diag/dpp"),
+    RT2_VARIANT(299, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, true); x.fair_prio = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/fair/diag/dpp"),
     // earlier choices of rounds 3-4 (the 5-product form before and after the threshold moved into the accumulator,
     // the first tile forms), kept for A/B; rounds 2-3's 16x16x32 and k16 kernels are in git history
     RT2_VARIANT(231, K_MFMA, render_mfma<kMfmaK5NoTn>, 256, "mfma/256/k5/notn/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"),

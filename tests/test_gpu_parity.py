@@ -130,8 +130,8 @@ def _last_variant(rt2mod, scene):
 
 
 AUTO_TILES = "mfmat5/768/k5/notn/tile19/coop0/w3/cmp/regs/cthr/perm"  # variant 293: > 8,192 triangles, LDS record tiles
-AUTO_RES = "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr"  # 282: <= 38 groups (1,216 triangles), records resident in LDS
-AUTO_RES_SLAB = "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/fair"  # 298: the same, < 6 items per lane (rank slabs)
+AUTO_RES = "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/dpp"  # 282: <= 38 groups (1,216 triangles), records resident in LDS
+AUTO_RES_SLAB = "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/fair/dpp"  # 298: the same, < 6 items per lane (rank slabs)
 AUTO_SMALL = "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp/cthr/yl1"  # 263: <= 8,192 triangles
 AUTO_SMALL_W3 = "mfma/256/k5/notn/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp/cthr"  # 262: packed fields too small
 
