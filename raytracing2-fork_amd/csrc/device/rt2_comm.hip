@@ -116,6 +116,9 @@ struct rt2_comm {
     DevBuf image, image8, rgb8;    // rt2_render_host_gather: root's whole image
     DevBuf status;                 // the agreement words (int32 x 2) on the device
     int32_t* hstatus = nullptr;    // ... and in pinned host memory (copies that never block the host)
+    hipEvent_t pre_gather = nullptr;       // rt2_gather_slabs: recorded on the caller's stream right before the
+    hipStream_t pre_gather_st = nullptr;   // gather, so rt2_comm_wait can tell this rank's own queued work (the
+    bool pre_gather_valid = false;         // render) from the collective
 };
 
 extern "C" int rt2_comm_unique_id(uint8_t* id) {
@@ -208,16 +211,34 @@ struct RcclTransport {
     // hold it up): waited for without a deadline, and its duration becomes
     // slack on the deadlines that follow — the next agreement also waits for
     // the slowest peer's render of an equal slab
-    int wait_local(hipStream_t st) {
+    // The local wait is still bounded (a kernel that never finishes must not
+    // hang this host forever while the peers time out): 20x RT2_COMM_TIMEOUT_S,
+    // then abort; a stream error aborts with HIP's message.
+    template <class Query>
+    int wait_local_q(Query query) {
         const auto t0 = std::chrono::steady_clock::now();
+        const double limit = 20.0 * comm_timeout_s();
         for (;;) {
-            const hipError_t q = hipStreamQuery(st);
+            const hipError_t q = query();
             if (q == hipSuccess) break;
-            if (q != hipErrorNotReady) return -1;
+            if (q != hipErrorNotReady) {
+                abort(std::string("stream error in this rank's own work before a collective: ") + hipGetErrorString(q));
+                return -1;
+            }
+            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
+                abort("this rank's own work before a collective ran longer than 20 x RT2_COMM_TIMEOUT_S");
+                return -1;
+            }
             std::this_thread::sleep_for(std::chrono::microseconds(50));
         }
         slack_s = 2.0 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         return 0;
+    }
+    int wait_local(hipStream_t st) {
+        return wait_local_q([&] { return hipStreamQuery(st); });
+    }
+    int wait_local_event(hipEvent_t ev) {
+        return wait_local_q([&] { return hipEventQuery(ev); });
     }
     // the agreement step: allreduce(max) of two ints on the communicator's own
     // stream, read back into pinned memory and waited for under the deadline;
@@ -304,6 +325,7 @@ extern "C" void rt2_comm_destroy(rt2_comm* c) {
                       &c->rgb8, &c->status})
         b->release();
     if (c->hstatus) (void)hipHostFree(c->hstatus);
+    if (c->pre_gather) (void)hipEventDestroy(c->pre_gather);
     if (c->owned && c->comm) (void)ncclCommDestroy(c->comm);  // null after an abort
     delete c;
 }
@@ -400,6 +422,13 @@ extern "C" int rt2_gather_slabs(rt2_comm* c, const void* d_slab, int32_t width, 
         return 0;
     };
     auto gather = [&]() -> int {
+        // everything queued on `st` before this point is this rank's own work
+        // (the render, the padding copy): rt2_comm_wait waits for it without
+        // the collective's deadline
+        if (!c->pre_gather && hipEventCreateWithFlags(&c->pre_gather, hipEventDisableTiming) != hipSuccess) return -1;
+        if (hipEventRecord(c->pre_gather, st) != hipSuccess) return -1;
+        c->pre_gather_st = st;
+        c->pre_gather_valid = true;
         return ncclGather(send, recv, slab_bytes, ncclUint8, root, c->comm, st) == ncclSuccess ? 0 : -1;
     };
     auto finish = [&](std::string& err) -> int {
@@ -427,6 +456,15 @@ extern "C" int rt2_comm_wait(rt2_comm* c, void* stream) {
     }
     HIPCHECK(hipSetDevice(c->device));
     RcclTransport t{c};
+    // the rank's own work queued before the last gather on this stream (its
+    // render: peers render alike) is waited for first, bounded but outside the
+    // deadline, and its duration becomes slack (a render longer than
+    // RT2_COMM_TIMEOUT_S must not abort a healthy job); then the deadline
+    // applies to the gather itself
+    if (c->pre_gather_valid && c->pre_gather_st == (hipStream_t)stream) {
+        c->pre_gather_valid = false;
+        if (t.wait_local_event(c->pre_gather) != 0) return -1;  // aborted and set the error
+    }
     return t.wait((hipStream_t)stream) == 0 ? 0 : -1;  // wait() aborted and set the error
 }
 

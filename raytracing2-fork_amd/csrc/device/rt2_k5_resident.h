@@ -1,9 +1,11 @@
-// The 5-product matrix filter without -tn and with the threshold in the
-// accumulator (rt2_mfma.h: MfmaSpec::k5 / no_tn / cthr) for scenes whose
-// records fit the LDS: every 32-triangle group's four record operands (U0,
-// V0, X0, T1: 4 KiB) are brought into the workgroup's LDS ONCE per launch and
-// every wave sweeps them from there for the rest of the launch.  Included by
-// rt2_render.hip only (one translation unit; internal linkage).
+// The matrix filter for scenes whose records fit the LDS: every 32-triangle
+// group's four record operands (4 KiB) are brought into the workgroup's LDS
+// ONCE per launch and every wave sweeps them from there for the rest of the
+// launch.  Two arithmetic forms (rt2_mfma.h): the 5-product form without -tn
+// with the threshold in the accumulator (MfmaSpec::k5 / no_tn / cthr: records
+// U0, V0, X0, T1 of the k16 layout; variants 282 / 298, round 5) and the
+// threshold in the K-slots (MfmaSpec::kthr: the kt records; round 6).
+// Included by rt2_render.hip only (one translation unit; internal linkage).
 //
 // Why: the 4-wave register kernel (render_mfma, variant 263) re-reads the
 // whole scene's records from L2 in every wave-segment — config B's 38 groups
@@ -14,7 +16,9 @@
 // traffic to L2 after the launch's first microseconds, no barrier after the
 // initial one (waves run free: each leaves when its own lanes are done and
 // the item pool is dry), and a group's operands are 4 conflict-free
-// ds_read_b128 per lane (~100 cycles) instead of L2 loads.
+// ds_read_b128 per lane (~100 cycles) instead of L2 loads.  MfmaSpec::res_l2
+// (kthr): a scene of more than res_groups groups keeps its first res_groups
+// resident and reads the rest per wave from L2 after them (up to 256 groups).
 //
 // The LDS then has no room for fragment rows, so the ray fragments are built
 // in registers: each lane forms its own ray's 16 k-slots (the rows' exact
@@ -23,10 +27,10 @@
 // blocks at once (frag_pair).  The Y fragment is rebuilt the same way when a
 // lane's bound improves: no LDS, no wave barrier.
 //
-// The arithmetic of every product, threshold and exact test is sweep_k16's
-// (5-product form, cthr) term for term, so the image is the sequential strict
-// `dst < best` scan's bit for bit.  Reference: compute.glsl:429-434 (the
-// `triangles[i]` loop this sweep replaces).
+// The filter only decides which (wave, triangle) pairs skip the exact test;
+// the exact phase is the reference arithmetic in index order, so the image is
+// the sequential strict `dst < best` scan's bit for bit.  Reference:
+// compute.glsl:429-434 (the `triangles[i]` loop this sweep replaces).
 #pragma once
 
 namespace {
@@ -37,15 +41,34 @@ struct K5Resident {
     h8 rec[NG * 4 * 64];
 };
 
-// Closest hit of every lane's ray over all triangles, records from LDS.
+// The exact phase of one group: the triangles with a passing pair (ballot M)
+// in index order, mt_pass3 + mt_exact (compute.glsl:302-340, strict `dst <
+// best`).  Returns whether some lane's bound improved.
+template <MfmaSpec S>
+__device__ __forceinline__ bool exact_group(unsigned long long M, int G, int n_tris, cfloat* tri, const f3& o,
+                                            const f3& d, float& best, int& bi, float& bestK, MfmaDiag& dg) {
+    if constexpr (S.diag) dg.hot += 1;
+    uint32_t m32 = (uint32_t)(M | M >> 32);
+    const float bk0 = bestK;
+    while (m32) {
+        const int tt = __builtin_ctz(m32);
+        m32 &= m32 - 1;
+        const int idx = 32 * G + tt;
+        if (idx >= n_tris) break;
+        if constexpr (S.diag) dg.exact += 1;
+        cfloat* tp = tri + 12 * idx;
+        const MtQ qq = mt_quantities(o, d, ldc4(tp), ldc4(tp + 4), ldc4(tp + 8));
+        if (mt_pass3(qq, bestK)) mt_exact(qq, idx, best, bi, bestK);
+    }
+    return __ballot(bestK != bk0) != 0;
+}
+
+// Closest hit of every lane's ray over all triangles, cthr records from LDS.
 // Returns false (wave-uniform, nothing computed) when a ray is outside the
 // filter's range.
 template <MfmaSpec S>
 __device__ __forceinline__ bool sweep_k5_res(const RenderParams& p, const h8* rec, const f3& o, const f3& d,
-                                             float& best, int& bi, float& bestK, MfmaDiag& dg, bool upper, int G0 = 0,
-                                             int G1 = -1) {
-    // [G0, G1): the 32-triangle groups to sweep (all by default; a range when
-    // the groups of one wave's segment are split into tail-job units)
+                                             float& best, int& bi, float& bestK, MfmaDiag& dg, bool upper) {
     static_assert(S.k5 && S.no_tn && S.cthr && S.ymma && S.imax && S.minred && S.ylds == 0, "the cthr 4-product form");
     const int lane = (int)lane_id();
     const f3 m = cross(d, o);
@@ -72,149 +95,84 @@ __device__ __forceinline__ bool sweep_k5_res(const RenderParams& p, const h8* re
     build_y(bestK);
     // MfmaSpec::thr_hoist: the threshold fragment once per sweep
     [[maybe_unused]] const h8 tfh = S.thr_hoist ? mfma_thr_frag(thr) : h8{};
-    const int ng = G1 < 0 ? (p.n_tris + 31) >> 5 : G1, n_tris = p.n_tris;
+    const int ng = (p.n_tris + 31) >> 5, n_tris = p.n_tris;
     cfloat* const tri = (cfloat*)p.tri;  // held across the sweep (not re-read from the kernel arguments per hot group)
-    const h8* tb = rec + (size_t)G0 * (4 * 64) + lane;
-    for (int G = G0; G < ng; G++) {
+    const h8* tb = rec + lane;
+    for (int G = 0; G < ng; G++) {
         const h8 b0 = tb[0], b2 = tb[64], b4 = tb[128], b6 = tb[192];
         tb += 4 * 64;
         const unsigned long long M = k5_cthr_group<S>(thr, a0, y1, b0, b2, b4, b6, upper, 0, tfh);
         if constexpr (S.diag) dg.groups += 1;
-        if (M) {
-            if constexpr (S.diag) dg.hot += 1;
-            // triangles of the group with a passing pair: the exact phase, in index order
-            uint32_t m32 = (uint32_t)(M | M >> 32);
-            const float bk0 = bestK;
-            while (m32) {
-                const int tt = __builtin_ctz(m32);
-                m32 &= m32 - 1;
-                const int idx = 32 * G + tt;
-                if (idx >= n_tris) break;
-                if constexpr (S.diag) dg.exact += 1;
-                cfloat* tp = tri + 12 * idx;
-                const MtQ qq = mt_quantities(o, d, ldc4(tp), ldc4(tp + 4), ldc4(tp + 8));
-                if (mt_pass3(qq, bestK)) mt_exact(qq, idx, best, bi, bestK);
-            }
-            if (__ballot(bestK != bk0)) build_y(bestK);
+        if (M && exact_group<S>(M, G, n_tris, tri, o, d, best, bi, bestK, dg)) build_y(bestK);
+    }
+    return true;
+}
+
+// The same with the threshold in the K-slots (MfmaSpec::kthr, kt records):
+// 8 independent products per group with a zero accumulator.  res_l2: groups
+// [res_groups, ng) are read from the scene's kt records in L2 after the
+// resident ones, in the same (index) order.
+template <MfmaSpec S>
+__device__ __forceinline__ bool sweep_kt_res(const RenderParams& p, const h8* rec, const f3& o, const f3& d,
+                                             float& best, int& bi, float& bestK, MfmaDiag& dg, bool upper) {
+    static_assert(S.kthr > 0 && S.ymma, "the kthr form");
+    const int lane = (int)lane_id();
+    const f3 m = cross(d, o);
+    MfmaScale sc;
+    if (!mfma_scale<S>(p.mfma_A, o, d, m, sc)) return false;
+    h8 a0[2], y1[2];
+    _Float16 tw16;
+    kt_frags<S>(d, m, sc, a0, tw16);
+    kt_y(d, o, bestK, sc, tw16, y1);
+    const int ng = (p.n_tris + 31) >> 5, n_tris = p.n_tris;
+    const int nres = S.res_l2 ? min(ng, S.res_groups) : ng;
+    cfloat* const tri = (cfloat*)p.tri;
+    const h8* tb = rec + lane;
+    for (int G = 0; G < nres; G++) {
+        const h8 b0 = tb[0], b1 = tb[64], b2 = tb[128], b3 = tb[192];
+        tb += kKtOps * 64;
+        const unsigned long long M = kt_group<S>(a0, y1, b0, b1, b2, b3, upper);
+        if constexpr (S.diag) dg.groups += 1;
+        if (M && exact_group<S>(M, G, n_tris, tri, o, d, best, bi, bestK, dg)) kt_y(d, o, bestK, sc, tw16, y1);
+    }
+    if constexpr (S.res_l2) {
+        const h8* gb = reinterpret_cast<const h8*>(p.mfma_kt_frag) + (size_t)nres * (kKtOps * 64) + lane;
+        for (int G = nres; G < ng; G++) {
+            const h8 b0 = gb[0], b1 = gb[64], b2 = gb[128], b3 = gb[192];
+            gb += kKtOps * 64;
+            const unsigned long long M = kt_group<S>(a0, y1, b0, b1, b2, b3, upper);
+            if constexpr (S.diag) dg.groups += 1;
+            if (M && exact_group<S>(M, G, n_tris, tri, o, d, best, bi, bestK, dg)) kt_y(d, o, bestK, sc, tw16, y1);
         }
     }
     return true;
 }
 
-// ---------------------------------------------------------------------------
-// Tail jobs (MfmaSpec::tail_jobs): once the item pool is dry, a wave whose
-// lanes are all done does not leave; it helps the waves of its workgroup that
-// still trace.  A pixel-frame's rays share one RNG stream, so a launch ends
-// with whole items whose segments run one after another on one lane; at the
-// end a lone wave sweeps all groups for its last few rays while the other
-// waves of its CU idle (the last ~13 % of a config B launch, more
-// of a 1/N rank slab).  A wave with <= 32 live rays (after compaction) posts
-// its segment as a JOB in the LDS left beside the records: its rays, a 64-bit
-// key per ray, and a ticket; the groups are cut into one unit per helper
-// (at most tail_jobs), which the helpers claim by compare-and-swap on the
-// ticket and sweep for the job's rays from scratch (bound = none), folding
-// each ray's result into its
-// key with an LDS atomic minimum on (dst bits << 32 | triangle index).  A hit
-// has dst > 1e-6 > 0, and positive binary32 values order like their bit
-// patterns, so the minimum key is the lexicographic (dst, index) minimum: the
-// smallest distance and, among exact ties, the lowest index — what the
-// sequential strict `dst < best` scan keeps.  Each unit's sweep starts from
-// no bound, for which the filter is still conservative (it only rejects what
-// the exact test rejects); the exact test is the reference arithmetic.  So
-// the result is bit-identical to the one-wave sweep (and to the oracle).
-// Termination: an owner posts only when helpers exist, and a helper leaves
-// only when no wave of the workgroup traces any more (busy == 0), which a wave
-// signals after its last job has completed; a claimed unit finishes without
-// waiting on anything, so the owner's wait for its units ends.  The owner
-// itself serves no unit: a form in which it served its own units (a call
-// inside its segment loop) returned correct keys but a corrupted image unless
-// further code followed the call — a code-generation effect around the call
-// that we did not isolate ("Tail jobs"); owners that only wait are
-// bit-exact.
-constexpr int kTailSlots = 6;  // jobs at once per workgroup (the LDS beside config B's 152 KiB of records)
-struct TailBoard {
-    float4 ray[kTailSlots][32][2];            // o (xyz), d (xyz) of the job's 32 rays (lanes 0..31 after compaction)
-    unsigned long long key[kTailSlots][32];   // (dst bits << 32 | index) minimum over the units; ~0 = no hit
-    uint32_t ticket[kTailSlots];              // epoch:24 | units:4 | next unit:4
-    uint32_t done[kTailSlots];                // units finished
-    uint32_t owner[kTailSlots];               // 0 = free, wave + 1
-    uint32_t busy;                            // waves of the workgroup that may still post jobs
-};
-__device__ __forceinline__ uint32_t lds_load_acq(uint32_t* a) {
-    return __hip_atomic_load(a, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// Sweeps unit u of nu of job j for the job's rays (lanes 0..31; lanes 32..63
-// carry ray 0, as a compacted owner's do) and folds the results into the keys.
-template <MfmaSpec S>
-__device__ __attribute__((noinline)) void serve_unit(const RenderParams& p, const h8* rec, TailBoard& tb, int j, int u,
-                                                    int nu, MfmaDiag& dg) {
-    const int lane = (int)lane_id(), src = lane < 32 ? lane : 0;
-    const float4 ro = tb.ray[j][src][0], rdv = tb.ray[j][src][1];
-    const f3 o = mk(ro.x, ro.y, ro.z), d = mk(rdv.x, rdv.y, rdv.z);
-    const int ng = (p.n_tris + 31) >> 5;
-    const int G0 = u * ng / nu, G1 = (u + 1) * ng / nu;
-    float best = 1e38f, bestK = 1e38f * 1.0009765625f;
-    int bi = -1;
-    (void)sweep_k5_res<S>(p, rec, o, d, best, bi, bestK, dg, false, G0, G1);  // in range: the owner checked these rays
-    if (lane < 32 && bi >= 0)
-        atomicMin(&tb.key[j][lane], (unsigned long long)__float_as_uint(best) << 32 | (uint32_t)bi);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane == 0) __hip_atomic_fetch_add(&tb.done[j], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// One claim on job j: the unit index (and the job's unit count), or -1 when
-// every unit is claimed.  Lane 0 runs the compare-and-swap; the outcome is
-// broadcast to the whole wave (wave-uniform control flow).
-__device__ __forceinline__ int claim_unit(TailBoard& tb, int j, int& nu) {
-    uint32_t got = 0xffffffffu;
-    if (lane_id() == 0) {
-        uint32_t t = lds_load_acq(&tb.ticket[j]);
-        while ((t & 15u) < ((t >> 4) & 15u)) {
-            if (__hip_atomic_compare_exchange_strong(&tb.ticket[j], &t, t + 1u, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
-                                                     __HIP_MEMORY_SCOPE_WORKGROUP)) {
-                got = t;
-                break;
-            }
-        }
-    }
-    got = (uint32_t)__builtin_amdgcn_readfirstlane((int)got);
-    if (got == 0xffffffffu) return -1;
-    nu = (int)((got >> 4) & 15u);
-    return (int)(got & 15u);
-}
-
 // render_mfma's segment loop (free-running waves: no barrier after the
-// records have landed) around sweep_k5_res.  The launcher takes it only for
-// scenes of at most S.res_groups groups (rt2_render).
+// records have landed) around sweep_k5_res / sweep_kt_res.  The launcher takes
+// it only for scenes of at most S.res_groups groups (res_l2: at most 256).
 template <MfmaSpec S>
 __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves))) void render_mfma_k5r(RenderParams p_arg) {
     static_assert(S.res_groups > 0 && !S.lockstep, "records resident in LDS; free-running waves");
+    static_assert(!S.res_l2 || S.kthr, "L2 groups beyond the resident ones: the kthr form");
     constexpr int NW = S.block / 64;
     __shared__ K5Resident<S.res_groups> rs;
-    [[maybe_unused]] TailBoard* tbp = nullptr;
-    if constexpr (S.tail_jobs > 0) {
-        __shared__ TailBoard board;
-        tbp = &board;
-        if (threadIdx.x < kTailSlots) {
-            board.ticket[threadIdx.x] = 0u;
-            board.done[threadIdx.x] = 0u;
-            board.owner[threadIdx.x] = 0u;
-        }
-        if (threadIdx.x == 0) board.busy = NW;
-    }
     {
-        // every group's 4 operands by LDS-DMA (1-KiB pieces, coalesced 16 B
-        // per lane, no VGPRs), dealt round-robin over the waves; then one
+        // every resident group's 4 operands by LDS-DMA (1-KiB pieces, coalesced
+        // 16 B per lane, no VGPRs), dealt round-robin over the waves; then one
         // barrier: every wave's pieces have landed
         const RenderParams& p = kargs<RenderParams>();
         const int ng = min((p.n_tris + 31) >> 5, S.res_groups);
-        const h8* gsrc = reinterpret_cast<const h8*>(p.mfma_k16_frag);
         const int lane = (int)lane_id(), wave = (int)(threadIdx.x >> 6);
         for (int pc = wave; pc < 4 * ng; pc += NW) {
-            const int gi = pc >> 2, op = 2 * (pc & 3);
-            __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void*)(gsrc + ((size_t)gi * kK16Ops + op) * 64 + lane),
-                (__attribute__((address_space(3))) void*)&rs.rec[pc * 64], 16, 0, 0);
+            const h8* src;
+            if constexpr (S.kthr)
+                src = reinterpret_cast<const h8*>(p.mfma_kt_frag) + (size_t)pc * 64 + lane;  // [G][4 ops] contiguous
+            else
+                src = reinterpret_cast<const h8*>(p.mfma_k16_frag) + ((size_t)(pc >> 2) * kK16Ops + 2 * (pc & 3)) * 64 +
+                      lane;  // ops 0, 2, 4, 6 of the k16 layout
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                             (__attribute__((address_space(3))) void*)&rs.rec[pc * 64], 16, 0, 0);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -222,8 +180,6 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
     Lane L;
     lane_init(L);
     MfmaDiag dg;
-    [[maybe_unused]] int slot = -1;          // tail jobs: this wave's job slot once it has one
-    [[maybe_unused]] uint32_t epoch = 0;
     const int wave = (int)(threadIdx.x >> 6);
     // diag wave timeline (p.wave_log, render_mfma's 10-word layout: start,
     // first lane out of items, end, segment rounds with two 32-ray blocks /
@@ -248,34 +204,7 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
                     wl_r2++;
             }
         }
-        if (!act) {
-            if constexpr (S.tail_jobs > 0) {
-                // every lane is done and the pool is dry: help the waves that
-                // still trace, until none does
-                TailBoard& tb = *tbp;
-                if (lane_id() == 0) {
-                    if (slot >= 0) __hip_atomic_store(&tb.owner[slot], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    __hip_atomic_fetch_add(&tb.busy, 0xffffffffu, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-                for (;;) {
-                    bool served = false;
-                    for (int j = 0; j < kTailSlots; j++) {
-                        int nu = 0;
-                        const int u = claim_unit(tb, j, nu);
-                        if (u >= 0) {
-                            serve_unit<S>(p, rs.rec, tb, j, u, nu, dg);
-                            served = true;
-                        }
-                    }
-                    if (!served) {
-                        const uint32_t b = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_load_acq(&tb.busy));
-                        if (b == 0) break;
-                        __builtin_amdgcn_s_sleep(2);
-                    }
-                }
-            }
-            break;
-        }
+        if (!act) break;  // every lane is done and the pool is dry
         if (__popcll(act) <= (unsigned)S.tail_lanes && __any(L.st == ST_DONE)) {
             float mybest = 1e38f;
             int mybi = -1;
@@ -338,61 +267,13 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
         const f3 ro = L.o, rd = L.d;
         float best = 1e38f, bestK = 1e38f * 1.0009765625f;
         int bi = -1;
-        bool swept = false;
-        if constexpr (S.tail_jobs > 0) {
-            // the pool is dry, <= 32 live rays (lanes 0..31), the rays in the
-            // filter's range, and the workgroup has waves that only help: the
-            // segment becomes a job of nu units
-            TailBoard& tb = *tbp;
-            const uint32_t helpers = NW - (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_load_acq(&tb.busy));
-            if (!upper && helpers > 0 && __any(L.st == ST_DONE) &&
-                !__ballot(!(abs_max3(ro) <= 0x1p20f && abs_max3(rd) <= 1.0001f))) {
-                if (slot < 0) {
-                    int got = -1;
-                    if (lane_id() == 0)
-                        for (int j = 0; j < kTailSlots && got < 0; j++) {
-                            uint32_t z = 0u;
-                            if (__hip_atomic_compare_exchange_strong(&tb.owner[j], &z, (uint32_t)wave + 1u,
-                                                                     __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
-                                                                     __HIP_MEMORY_SCOPE_WORKGROUP))
-                                got = j;
-                        }
-                    slot = __builtin_amdgcn_readfirstlane(got);
-                    if (slot >= 0) epoch = lds_load_acq(&tb.ticket[slot]) >> 8;
-                }
-                if (slot >= 0) {
-                    const int j = slot;
-                    const int nu = (int)min((uint32_t)S.tail_jobs, helpers);
-                    if (lane_id() < 32) {
-                        tb.ray[j][lane_id()][0] = make_float4(ro.x, ro.y, ro.z, 0.0f);
-                        tb.ray[j][lane_id()][1] = make_float4(rd.x, rd.y, rd.z, 0.0f);
-                        tb.key[j][lane_id()] = ~0ull;
-                    }
-                    epoch = (epoch + 1u) & 0xffffffu;
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    if (lane_id() == 0) {
-                        __hip_atomic_store(&tb.done[j], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        __hip_atomic_store(&tb.ticket[j], epoch << 8 | (uint32_t)nu << 4, __ATOMIC_RELEASE,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-                    }
-                    // the helpers serve the units; each claimed unit finishes
-                    // without waiting on anything
-                    while ((uint32_t)__builtin_amdgcn_readfirstlane((int)lds_load_acq(&tb.done[j])) < (uint32_t)nu)
-                        __builtin_amdgcn_s_sleep(1);
-                    if (lane_id() < 32) {
-                        const unsigned long long k = tb.key[j][lane_id()];
-                        if (k != ~0ull) {
-                            best = __uint_as_float((uint32_t)(k >> 32));
-                            bi = (int)(uint32_t)k;
-                        }
-                    }
-                    swept = true;
-                }
-            }
-        }
+        bool swept;
+        if constexpr (S.kthr)
+            swept = sweep_kt_res<S>(p, rs.rec, ro, rd, best, bi, bestK, dg, upper);
+        else
+            swept = sweep_k5_res<S>(p, rs.rec, ro, rd, best, bi, bestK, dg, upper);
         // a ray outside the filter's range (wave-uniform): the drain's code
-        if (!swept && !sweep_k5_res<S>(p, rs.rec, ro, rd, best, bi, bestK, dg, upper))
-            coop_each(act, ro, rd, p, best, bi);
+        if (!swept) coop_each(act, ro, rd, p, best, bi);
         if (mine) {
             L.bounce += 1;
             L.segs += 1;

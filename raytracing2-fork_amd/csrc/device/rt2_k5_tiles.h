@@ -67,7 +67,7 @@ __device__ __forceinline__ void wait_vm(int n) {
 // rays are outside the filter's range (nothing computed; wave-uniform).
 template <MfmaSpec S, class SH>
 __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, SH& sh,
-                                               K5Tiles<S.tile_groups, S.tile_bufs, !S.cthr>& tl,
+                                               K5Tiles<S.tile_groups, S.tile_bufs, !(S.cthr || S.kthr)>& tl,
                                                const f3& o, const f3& d, float& best, int& bi, float& bestK,
                                                MfmaDiag& dg, bool sweeping, bool upper) {
     static_assert(S.k5 && S.ymma && S.imax && S.minred && S.tile_groups > 0, "the 5-product form");
@@ -81,8 +81,13 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, SH& sh,
     float zlo = 0.0f, zhi = 0.0f;
     h8 a0[2], a1[2], y1[2];
     [[maybe_unused]] ThrBits thr = {};
+    [[maybe_unused]] _Float16 tw16 = (_Float16)0.0f;  // kthr: Tw' for the Y rebuilds
     bool compute = false, in_range = true;
     auto write_y = [&](float bkv) {
+        if constexpr (S.kthr) {
+            kt_y(d, o, bkv, sc, tw16, y1);
+            return;
+        }
         _Float16 s[16];
         mfma_y_chunk(s, d, o, bkv, sc.sigma, sc.Bmax);
         if constexpr (S.perm_frag) {
@@ -102,7 +107,12 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, SH& sh,
     if (sweeping) {
         const f3 m = cross(d, o);
         in_range = mfma_scale<S>(p.mfma_A, o, d, m, sc);
-        if (in_range && S.perm_frag) {
+        if (in_range && S.kthr) {
+            // MfmaSpec::kthr: the threshold in the K-slots (register fragments)
+            kt_frags<S>(d, m, sc, a0, tw16);
+            write_y(bestK);
+            compute = true;
+        } else if (in_range && S.perm_frag) {
             // MfmaSpec::perm_frag: the fragments built in registers by
             // v_permlane32_swap (rt2_k5_resident.h frag_pair), no LDS rows
             _Float16 s[18];
@@ -142,7 +152,7 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, SH& sh,
         }
     }
     const int ng = (p.n_tris + 31) >> 5, nt = (ng + K - 1) / K;
-    const h8* gsrc = reinterpret_cast<const h8*>(p.mfma_k16_frag);
+    const h8* gsrc = reinterpret_cast<const h8*>(S.kthr ? p.mfma_kt_frag : p.mfma_k16_frag);
     // LDS-DMA of tile t into buffer t % NB, round-robin over the waves: 4 record
     // pieces per group (1 KiB each: a lane's 16 B land at base + 16 lane),
     // then the groups' bounds (256 B per group) and scales (128 B per group)
@@ -150,15 +160,15 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, SH& sh,
     auto issue = [&](int t) {
         const int g0 = t * K, gn = min(K, ng - g0);
         // cthr: the -tn record carries the threshold; no bounds or scales
-        const int nrec = gn * 4, nbnd = S.cthr ? 0 : (gn * 16 + 63) / 64, ntau = S.cthr ? 0 : (gn * 8 + 63) / 64;
+        const int nrec = gn * 4, nbnd = (S.cthr || S.kthr) ? 0 : (gn * 16 + 63) / 64, ntau = (S.cthr || S.kthr) ? 0 : (gn * 8 + 63) / 64;
         const int b = t % NB;
         for (int pc = wave; pc < nrec + nbnd + ntau; pc += NW) {
             if (pc < nrec) {
-                const int gi = pc >> 2, op = 2 * (pc & 3);
+                const int gi = pc >> 2, op = S.kthr ? (pc & 3) : 2 * (pc & 3);  // kt: 4 contiguous ops per group
                 __builtin_amdgcn_global_load_lds(
-                    (const __attribute__((address_space(1))) void*)(gsrc + ((size_t)(g0 + gi) * kK16Ops + op) * 64 + lane),
+                    (const __attribute__((address_space(1))) void*)(gsrc + ((size_t)(g0 + gi) * (S.kthr ? kKtOps : kK16Ops) + op) * 64 + lane),
                     (__attribute__((address_space(3))) void*)&tl.rec[b][pc * 64], 16, 0, 0);
-            } else if constexpr (S.cthr) {
+            } else if constexpr (S.cthr || S.kthr) {
                 // (no bound or scale pieces)
             } else if (pc < nrec + nbnd) {
                 const int q = pc - nrec;
@@ -182,7 +192,7 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, SH& sh,
     // this wave's pieces of tile t (issued round-robin: pc = wave, wave + NW, ...)
     auto my_pieces = [&](int t) {
         const int gn = min(K, ng - t * K);
-        const int n = gn * 4 + (S.cthr ? 0 : (gn * 16 + 63) / 64 + (gn * 8 + 63) / 64);
+        const int n = gn * 4 + ((S.cthr || S.kthr) ? 0 : (gn * 16 + 63) / 64 + (gn * 8 + 63) / 64);
         return wave < n ? (n - wave + NW - 1) / NW : 0;
     };
     for (int t = 0; t < NB - 1 && t < nt; t++) issue(t);
@@ -209,7 +219,7 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, SH& sh,
             nb[1] = tb[64];
             nb[2] = tb[128];
             nb[3] = tb[192];
-            if constexpr (!S.cthr) {
+            if constexpr (!(S.cthr || S.kthr)) {
                 ntau = tl.tau[b][gi * 32 + r32];
                 nbnd = tl.bnd[b][gi * 32 + r32];
             }
@@ -227,7 +237,9 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, SH& sh,
             // slots, padded by 2^-10 for its own rounding ("The
             // 5-product form")
             unsigned long long M;
-            if constexpr (S.cthr) {
+            if constexpr (S.kthr) {
+                M = kt_group<S>(a0, y1, b0, b2, b4, b6, upper);
+            } else if constexpr (S.cthr) {
                 M = k5_cthr_group<S>(thr, a0, y1, b0, b2, b4, b6, upper, sh);
             } else {
             const float Tl = tau * sc.Tw + (bnd.x * zlo + bnd.y * zhi) * 1.0009765625f;
@@ -314,7 +326,7 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
     // MfmaSpec::perm_frag: no fragment rows (one row array serves as a dummy
     // the sweep never touches)
     __shared__ WL wl[S.perm_frag ? 1 : NW];
-    __shared__ K5Tiles<S.tile_groups, S.tile_bufs, !S.cthr> tl;
+    __shared__ K5Tiles<S.tile_groups, S.tile_bufs, !(S.cthr || S.kthr)> tl;
     __shared__ BlockVote<NW> vote;
     uint32_t vote_parity = 0;
     WL& sh = wl[S.perm_frag ? 0 : threadIdx.x >> 6];

@@ -79,12 +79,19 @@ struct MfmaSpec {
                             // product per group, mfma_thr_frag), and the reduction is a sign-bit AND / OR
                             // (2 v_bitop3_b32 per pair instead of 2.5 min / max)
     bool perm_frag = false; // render_mfma_k5t: fragments built in registers by v_permlane32_swap (no LDS rows)
-    int tail_jobs = 0;      // render_mfma_k5r: up to this many units per tail job (0 = no tail jobs)
     bool thr_hoist = false;  // k5_cthr_group: the threshold fragment built once per sweep, not once per group
     bool fair_prio = false;  // render_mfma_k5r: issue priority (s_setprio) by the rays the wave's slowest lane has
                              // left, quartiles of the rays per pixel (fair share among a SIMD's waves)
     int res_groups = 0;     // render_mfma_k5r (rt2_k5_resident.h): every group's records resident in the
                             // workgroup's LDS for the whole launch (scenes of <= res_groups 32-triangle groups)
+    int kthr = 0;           // the threshold in the K-slots (round 6, DESIGN.md "The threshold in the K-slots"):
+                            // U, -V, X drop the m.y and m.z cross slots and carry -tau x Tw' and -B x W' in slots
+                            // 14, 15; Y carries -tau x Tw' in slot 29: 8 products per group with a zero
+                            // accumulator, no TT product.  Schedule per 32-ray block: 1 = the four products, then
+                            // the 32 sign-bit VALU; 2 = U V X | their AND | Y | the fold (cthr's order); 3 = no
+                            // fences (the compiler's order)
+    bool res_l2 = false;    // render_mfma_k5r + kthr: groups beyond res_groups are read from L2 (global loads per
+                            // wave) after the resident ones: scenes of up to 256 groups
     int sol = 0;            // speed-of-light probes (WRONG images; diag clocks only): 1 = every group reads group
                             // 0's records, 2 = no exact phase, 3 = 2 + only the U term is reduced; marginal-cost
                             // probes (same image): 4 = exact phase twice, 5 = products and reduction twice,
@@ -789,6 +796,149 @@ __device__ __forceinline__ unsigned long long k5_cthr_group(ThrBits tb, const h8
     return __ballot(acc < 0);
 }
 
+// ---------------------------------------------------------------------------
+// MfmaSpec::kthr — the threshold in the K-slots (round 6; DESIGN.md "The
+// threshold in the K-slots").  The cthr form spends a tenth matrix product per
+// group on TT = -Tl'' and holds its 16 VGPRs live as the accumulator operand of
+// every other product, which also chains U, -V, X and Y behind it.  Here the
+// threshold is two more k-slots of the products themselves:
+//   - U, -V, X keep d (9 slots), m.x (3) and the hi x hi products of m.y and
+//     m.z; the four cross slots of m.y and m.z (coefficient hi x ray lo,
+//     coefficient lo x ray hi) are left out and bounded, per component c, by
+//     2^-10 CT_c mw_c with CT_c = max(|c_hi|, 2^11 |c_lo|) (triangle) and
+//     mw_c = max(|r_hi|, 2^11 |r_lo|) (ray): |c_hi r_lo| <= CT 2^-11 mw and
+//     |c_lo r_hi| <= 2^-11 CT mw.  Summed over y and z, <= B_q W with
+//     B_q = 2^-10 max(CT_y, CT_z) of the quantity's own coefficients and
+//     W = max over the wave of (mw_y + mw_z);
+//   - slot 14 carries -tau against Tw' = Tw (1 + 2^-8) rounded up to f16, and
+//     slot 15 -B_q (rounded up in magnitude) against W' = W (1 + 2^-8) rounded
+//     up, so each product comes out as its kept sum minus (tau Tw' + B_q W');
+//   - Y's fragment carries Tw' in slot 29 against the -tn record's -tau.
+// A pair passes iff all four terms are negative (the sign-bit AND of the cthr
+// form); the 8 products per group take a zero accumulator and are independent.
+// Records: [32-group][4: U, -V, X (first K-half), T1 (-tn second half)][64][8].
+constexpr int kKtOps = 4;
+__global__ void prep_mfma_kt(const float4* tri, int n, int n_pad, _Float16* out, uint32_t* flags) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_pad) return;
+    MfmaCoef k;
+    mfma_coefs(tri, i, n, k, flags);
+    const int G = i >> 5, t = i & 31;
+    for (int op = 0; op < kKtOps; op++) {
+        _Float16 slot[32], h[16];
+        if (op < 3) {
+            mfma_slots(k.c[op], k.tau, slot);
+            // slots 12, 13, 14: m.y (hi, hi, lo); 15, 16, 17: m.z (hi, hi, lo)
+            const float ct = fmaxf(fmaxf(fabsf((float)slot[12]), 2048.0f * fabsf((float)slot[14])),
+                                   fmaxf(fabsf((float)slot[15]), 2048.0f * fabsf((float)slot[17])));
+            for (int j = 0; j < 13; j++) h[j] = slot[j];  // d (0..8), m.x (9..11), m.y hi x hi (12)
+            h[13] = slot[15];                             // m.z hi x hi
+            h[14] = (_Float16)(float)-k.tau;              // a power of two in [2^-9, 2^13]: exact
+            h[15] = -f16_up(ct * 0x1p-10f);               // B_q, rounded up in magnitude
+        } else {
+            mfma_slots(k.c[3], k.tau, slot);
+            for (int j = 0; j < 16; j++) h[j] = slot[16 + j];  // o (18..26), the constant (27, 28)
+            h[13] = (_Float16)(float)-k.tau;                    // slot 29 against Y's Tw'
+            h[14] = h[15] = (_Float16)0.0f;
+        }
+        for (int j = 0; j < 16; j++) out[((size_t)(G * kKtOps + op) * 64 + t + 32 * (j >> 3)) * 8 + (j & 7)] = h[j];
+    }
+}
+
+// This lane's first K-half of the kthr main fragment: d and m.x as (hi, lo,
+// hi), m.y hi, m.z hi; slots 14, 15 (Tw', W') are wave-uniform and filled by
+// the caller.  Returns the lane's mw_y + mw_z.
+__device__ __forceinline__ float kt_main_slots(_Float16 s[16], const f3& d, const f3& m, float sigma) {
+    const float comp[4] = {d.x, d.y, d.z, m.x};
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const float v = comp[c] * sigma;
+        const _Float16 hi = (_Float16)v;
+        const _Float16 lo = (_Float16)(v - (float)hi);
+        s[3 * c] = hi;
+        s[3 * c + 1] = lo;
+        s[3 * c + 2] = hi;
+    }
+    float W = 0.0f;
+    const float yz[2] = {m.y, m.z};
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+        const float v = yz[c] * sigma;
+        const _Float16 hi = (_Float16)v;
+        const _Float16 lo = (_Float16)(v - (float)hi);
+        s[12 + c] = hi;
+        W += fmaxf(fabsf((float)hi), 2048.0f * fabsf((float)lo));
+    }
+    return W;
+}
+
+// The wave's kthr fragments: a0 (both 32-ray blocks' first K-half with the
+// threshold factors) and y1 via frag_pair; tw16 keeps Tw' for the Y rebuilds.
+template <MfmaSpec S>
+__device__ __forceinline__ void kt_frags(const f3& d, const f3& m, const MfmaScale& sc, h8 a0[2], _Float16& tw16) {
+    constexpr float pad = 1.00390625f;  // 1 + 2^-8 (the f32 sum mw_y + mw_z and the scale product round)
+    _Float16 s[16];
+    const float W = wave_max_s<S>(kt_main_slots(s, d, m, sc.sigma));
+    tw16 = f16_up(sc.Tw * pad);
+    s[14] = tw16;
+    s[15] = f16_up(W * pad);
+    frag_pair(s, a0);
+}
+__device__ __forceinline__ void kt_y(const f3& d, const f3& o, float bkv, const MfmaScale& sc, _Float16 tw16,
+                                     h8 y1[2]) {
+    _Float16 s[16];
+    mfma_y_chunk(s, d, o, bkv, sc.sigma, sc.Bmax);
+    s[13] = tw16;  // slot 29: Tw' against the record's -tau
+    frag_pair(s, y1);
+}
+
+// One group's filter for the wave's one or two 32-ray blocks (records bu, bv,
+// bx: U, -V, X; bt: the -tn record's second K-half).  Returns the ballot of
+// lanes whose triangle has a passing pair.
+template <MfmaSpec S>
+__device__ __forceinline__ unsigned long long kt_group(const h8* a0, const h8* y1, const h8& bu, const h8& bv,
+                                                       const h8& bx, const h8& bt, bool upper) {
+    static_assert(S.kthr >= 1 && S.kthr <= 3, "kthr schedule");
+    const f16v zero = {};
+    int acc = 0;
+#pragma unroll
+    for (int R = 0; R < 2; R++) {
+        if (R == 1 && !upper) break;
+        const f16v U = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[R], bu, zero, 0, 0, 0);
+        const f16v V = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[R], bv, zero, 0, 0, 0);
+        const f16v X = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[R], bx, zero, 0, 0, 0);
+        if constexpr (S.kthr == 1) {
+            // the four products first, then the 32 sign-bit VALU (scheduling
+            // groups: a plain sched_barrier between them does not hold, the
+            // products are pure and the DAG places Y after the AND)
+            const f16v Y = __builtin_amdgcn_mfma_f32_32x32x16_f16(y1[R], bt, zero, 0, 0, 0);
+            int t3[16];
+#pragma unroll
+            for (int i = 0; i < 16; i++)
+                t3[i] = __builtin_amdgcn_bitop3_b32(__float_as_int(U[i]), __float_as_int(V[i]), __float_as_int(X[i]), 0x80);
+#pragma unroll
+            for (int i = 0; i < 16; i++) acc = __builtin_amdgcn_bitop3_b32(t3[i], __float_as_int(Y[i]), acc, 0xEA);
+            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);   // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 32, 0);  // VALU
+            __builtin_amdgcn_sched_barrier(0);
+        } else {
+            if constexpr (S.kthr == 2) __builtin_amdgcn_sched_barrier(0);
+            int t3[16];
+#pragma unroll
+            for (int i = 0; i < 16; i++)
+                t3[i] = __builtin_amdgcn_bitop3_b32(__float_as_int(U[i]), __float_as_int(V[i]), __float_as_int(X[i]), 0x80);
+            if constexpr (S.kthr == 2) __builtin_amdgcn_sched_barrier(0);
+            const f16v Y = __builtin_amdgcn_mfma_f32_32x32x16_f16(y1[R], bt, zero, 0, 0, 0);
+            if constexpr (S.kthr == 2) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 16; i++) acc = __builtin_amdgcn_bitop3_b32(t3[i], __float_as_int(Y[i]), acc, 0xEA);
+            if constexpr (S.kthr == 2)
+                if (R == 1) __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    return __ballot(acc < 0);
+}
+
 __device__ __forceinline__ f16v Y_unused_init() { return f16v{}; }
 template <MfmaSpec S, class SH>
 __device__ __forceinline__ bool sweep_k16(const RenderParams& p, SH& sh, const f3& o, const f3& d, float& best,
@@ -1119,9 +1269,73 @@ __global__ __launch_bounds__(64) void mfma_probe_kernel(RenderParams p, const fl
         for (int j = 0; j < 16; j++) sh.ray[lane][32 + j] = s[j];
     }
     __syncthreads();
-    for (int j = 0; j < 48; j++) frags[ray * 48 + j] = sh.ray[lane][j];
+    for (int j = 0; j < 48; j++) frags[ray * 80 + j] = sh.ray[lane][j];
     const size_t ray0 = (size_t)blockIdx.x * 64;
-    if constexpr (S.k16) {
+    if constexpr (S.perm_frag) {
+        // the shipping kernels' operand path (282 / 293 / 298 and the kthr
+        // kernels): fragments built in registers by frag_pair, not read from
+        // LDS rows.  frags[ray][48..63] receives the main fragment and
+        // [64..79] the Y fragment as the MFMA A operand holds them (block R,
+        // lane l: ray 32R + (l & 31), k-slots 8 (l >> 5) .. +7), so the host
+        // can check the permutation against the rows above.
+        const int r32 = lane & 31, hl = lane >> 5;
+        h8 a0[2], y1[2];
+        [[maybe_unused]] ThrBits tb = {};
+        [[maybe_unused]] _Float16 tw16 = (_Float16)0.0f;
+        if constexpr (S.kthr) {
+            kt_frags<S>(d, m, sc, a0, tw16);
+            kt_y(d, o, bestK, sc, tw16, y1);
+        } else {
+            _Float16 s[18];
+            mfma_main_half_slots(s, d, m, sc.sigma);
+            frag_pair(s, a0);
+            _Float16 t[16];
+            mfma_y_chunk(t, d, o, bestK, sc.sigma, sc.Bmax);
+            frag_pair(t, y1);
+            const float vz = m.z * sc.sigma;
+            const _Float16 hz = (_Float16)vz;
+            const _Float16 lz = (_Float16)(vz - (float)hz);
+            tb = mfma_thr_bits(sc.Tw, wave_max(fabsf((float)lz)), wave_max(fabsf((float)hz)));
+        }
+        for (int R = 0; R < 2; R++)
+            for (int j = 0; j < 8; j++) {
+                frags[(ray0 + 32 * R + r32) * 80 + 48 + 8 * hl + j] = a0[R][j];
+                frags[(ray0 + 32 * R + r32) * 80 + 64 + 8 * hl + j] = y1[R][j];
+            }
+        const h8* fg = reinterpret_cast<const h8*>(S.kthr ? p.mfma_kt_frag : p.mfma_k16_frag) + lane;
+        const int nops = S.kthr ? kKtOps : kK16Ops;
+        const f16v zero = {};
+        for (int G = 0; G < n_pad / 32; G++) {
+            h8 b[kK16Ops];
+            for (int op = 0; op < nops; op++) b[op] = fg[(size_t)G * nops * 64 + 64 * op];
+            for (int R = 0; R < 2; R++) {
+                K16Terms q;
+                if constexpr (S.kthr) {
+                    q.U = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[R], b[0], zero, 0, 0, 0);
+                    q.V = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[R], b[1], zero, 0, 0, 0);
+                    q.X = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[R], b[2], zero, 0, 0, 0);
+                    q.T = zero;
+                    q.Y = __builtin_amdgcn_mfma_f32_32x32x16_f16(y1[R], b[3], zero, 0, 0, 0);
+                } else {
+                    const f16v c = __builtin_amdgcn_mfma_f32_32x32x16_f16(mfma_thr_frag(tb), b[6], zero, 0, 0, 0);
+                    q.U = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[R], b[0], c, 0, 0, 0);
+                    q.V = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[R], b[2], c, 0, 0, 0);
+                    q.X = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[R], b[4], c, 0, 0, 0);
+                    q.T = c;
+                    q.Y = __builtin_amdgcn_mfma_f32_32x32x16_f16(y1[R], b[6], c, 0, 0, 0);
+                }
+                for (int i = 0; i < 16; i++) {
+                    const size_t rr = ray0 + 32 * R + 8 * (i >> 2) + 4 * hl + (i & 3);
+                    float* tt = terms + (rr * n_pad + 32 * G + r32) * 5;
+                    tt[0] = q.U[i];
+                    tt[1] = q.V[i];
+                    tt[2] = q.X[i];
+                    tt[3] = q.T[i];
+                    tt[4] = q.Y[i];
+                }
+            }
+        }
+    } else if constexpr (S.k16) {
         const int r32 = lane & 31, hl = lane >> 5;
         // MfmaSpec::cthr: the sweep's threshold factors (the wave's m.z halves)
         [[maybe_unused]] ThrBits tb = {};

@@ -79,6 +79,7 @@ struct rt2_scene {
     _Float16* d_mfma_k16 = nullptr;             // sweep_k16 records (32-triangle groups, 7 KiB each)
     float* d_mfma_k16_tau = nullptr;            // per-triangle record scale (same values as d_mfma_tau)
     float2* d_mfma_k16_bnd = nullptr;           // per-triangle m.z residual bounds of the 5-product form (k5)
+    _Float16* d_mfma_kt = nullptr;              // kthr records (threshold in the K-slots: 4 KiB per 32 triangles)
     int mfma_ok = 0;                            // render_mfma usable (records built, scene in range)
     float mfma_A = 0.0f;                        // max |a_i| over the in-range triangles
     float4* d_fb = nullptr;                     // frame_split scratch (per-frame colours)
@@ -430,6 +431,14 @@ static int scene_init(rt2_scene* s, const rt2_triangle* tris, int32_t n_tris, co
         HIPCHECK(hipMemset(d_mflags, 0, 2 * sizeof(uint32_t)));
         std::memcpy(&s->mfma_A, &mflags[1], sizeof(float));
         s->mfma_ok = s->mfma_A <= 0x1p20f;
+        // the kthr records (rt2_mfma.h prep_mfma_kt: the threshold in the
+        // K-slots), 4 KiB per 32 triangles; its flags duplicate the above
+        HIPCHECK(hipMalloc(&s->d_mfma_kt, (size_t)n_pad32 * kKtOps * 16 * sizeof(_Float16)));
+        hipLaunchKernelGGL(prep_mfma_kt, dim3((n_pad32 + 255) / 256), dim3(256), 0, 0, s->d_tri, n_tris, n_pad32,
+                           s->d_mfma_kt, d_mflags);
+        HIPCHECK(hipGetLastError());
+        HIPCHECK(hipDeviceSynchronize());
+        HIPCHECK(hipMemset(d_mflags, 0, 2 * sizeof(uint32_t)));
     }
     HIPCHECK(hipDeviceSynchronize());
     return 0;
@@ -470,6 +479,7 @@ extern "C" void rt2_scene_destroy(rt2_scene* s) {
     (void)hipFree(s->d_mfma_k16);
     (void)hipFree(s->d_mfma_k16_tau);
     (void)hipFree(s->d_mfma_k16_bnd);
+    (void)hipFree(s->d_mfma_kt);
     (void)hipFree(s->d_fb);
     (void)hipFree(s->d_cost);
     (void)hipFree(s->d_order);
@@ -609,7 +619,7 @@ constexpr MfmaSpec k5_tiles_spec(int K, bool no_tn, int tail, bool diag = false)
 // records resident in LDS (rt2_k5_resident.h): one workgroup per CU (3 or 4
 // waves per SIMD), scenes of <= kResGroups 32-triangle groups
 constexpr int kResGroups = 38;  // 152 KiB of k5 records (4 KiB per group) of the CU's 160 KiB
-constexpr MfmaSpec k5_res_spec(int waves, bool diag = false, int tail = 4, int jobs = 0) {
+constexpr MfmaSpec k5_res_spec(int waves, bool diag = false, int tail = 4) {
     MfmaSpec x = kMfmaK5NoTn;
     x.block = 256 * waves;
     x.waves = waves;
@@ -617,13 +627,35 @@ constexpr MfmaSpec k5_res_spec(int waves, bool diag = false, int tail = 4, int j
     x.lane_lds = 0;
     x.cthr = true;
     x.lockstep = false;
-    x.tail_jobs = jobs;
     x.thr_hoist = true;  // the threshold fragment once per sweep (config B 158.9 vs 160.2, 166.3 vs 167.5 ms)
     x.dpp = true;        // the segment's wave maxima by DPP lane moves (159.4 vs 160.4, 163.1 vs 164.6 ms)
     x.res_groups = kResGroups;
     x.diag = diag;
     return x;
 }
+// the threshold in the K-slots (round 6, MfmaSpec::kthr): the resident kernel on the kt records, schedule `sched`;
+// l2: scenes of up to 256 groups, the groups beyond the resident 38 read from L2
+constexpr MfmaSpec kt_res_spec(int sched, bool diag = false, bool l2 = false) {
+    MfmaSpec x = k5_res_spec(4, diag);
+    x.cthr = false;
+    x.thr_hoist = false;
+    x.kthr = sched;
+    x.res_l2 = l2;
+    return x;
+}
+// ... and the LDS-tiled kernel on the kt records (the form of 293), K groups per tile, `waves` per SIMD
+constexpr MfmaSpec kt_tiles_spec(int K, int waves, int sched) {
+    MfmaSpec x = k5_tiles_spec(K, true, 0);
+    x.block = 256 * waves;
+    x.waves = waves;
+    x.rows80 = true;
+    x.lane_lds = 0;
+    x.perm_frag = true;
+    x.dpp = true;
+    x.kthr = sched;
+    return x;
+}
+constexpr int kResL2Groups = 256;  // render_mfma_k5r with res_l2: 38 groups resident, the rest from L2
 constexpr Bvh3Spec kBvhDefault{.block = 256, .thresh = 16, .slab = Slab::Markstein, .waves = 5, .diag = false};
 
 #ifdef RT2_EXPERIMENTS
@@ -666,11 +698,23 @@ const Variant kVariants[] = {
     // tiles hold 19 groups
     RT2_VARIANT(293, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(19, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; x.perm_frag = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile19/coop0/w3/cmp/regs/cthr/perm"),
 #ifdef RT2_EXPERIMENTS
-    // records resident in LDS at 3 waves per SIMD; tail jobs (DESIGN.md "Tail jobs", measured slower); the
-    // resident kernel's diagnostic counters
+    // records resident in LDS at 3 waves per SIMD; the resident kernel's diagnostic counters
     RT2_VARIANT(280, K_MFMA, render_mfma_k5r<k5_res_spec(3)>, 768, "mfmar/768/k5/notn/res38/coop4/w3/cmp/cthr/dpp"),
-    RT2_VARIANT(288, K_MFMA, render_mfma_k5r<k5_res_spec(4, false, 4, 8)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/jobs8/dpp"),
     RT2_VARIANT(287, K_MFMA, render_mfma_k5r<k5_res_spec(4, true)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/diag/dpp"),
+    // the threshold in the K-slots (round 6): schedules 1 (four products, then the reduction) / 2 (cthr's order) /
+    // 3 (no fences); fair-share priority; diagnostic counters; the L2 continuation for 39..256 groups
+    RT2_VARIANT(320, K_MFMA, render_mfma_k5r<kt_res_spec(1)>, 1024, "mfmar/1024/kt1/res38/coop4/w4/cmp/dpp"),
+    RT2_VARIANT(321, K_MFMA, render_mfma_k5r<kt_res_spec(2)>, 1024, "mfmar/1024/kt2/res38/coop4/w4/cmp/dpp"),
+    RT2_VARIANT(322, K_MFMA, render_mfma_k5r<kt_res_spec(3)>, 1024, "mfmar/1024/kt3/res38/coop4/w4/cmp/dpp"),
+    RT2_VARIANT(323, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = kt_res_spec(1); x.fair_prio = true; return x; }()>, 1024, "mfmar/1024/kt1/res38/coop4/w4/cmp/fair/dpp"),
+    RT2_VARIANT(324, K_MFMA, render_mfma_k5r<kt_res_spec(1, true)>, 1024, "mfmar/1024/kt1/res38/coop4/w4/cmp/diag/dpp"),
+    RT2_VARIANT(325, K_MFMA, render_mfma_k5r<kt_res_spec(1, false, true)>, 1024, "mfmarl2/1024/kt1/res38l2/coop4/w4/cmp/dpp"),
+    // ... on the LDS-tiled kernel (the form of 293): 19-group tiles at 3 waves per SIMD (schedules 1, 2), 16-group
+    // tiles at 4 waves
+    RT2_VARIANT(330, K_MFMA, render_mfma_k5t<kt_tiles_spec(19, 3, 1)>, 768, "mfmat5/768/kt1/tile19/coop0/w3/cmp/regs/perm"),
+    RT2_VARIANT(331, K_MFMA, render_mfma_k5t<kt_tiles_spec(19, 3, 2)>, 768, "mfmat5/768/kt2/tile19/coop0/w3/cmp/regs/perm"),
+    RT2_VARIANT(333, K_MFMA, render_mfma_k5t<kt_tiles_spec(16, 4, 1)>, 1024, "mfmat5/1024/kt1/tile16/coop0/w4/cmp/regs/perm"),
+    RT2_VARIANT(334, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 1); x.diag = true; return x; }()>, 768, "mfmat5/768/kt1/tile19/coop0/w3/cmp/regs/perm/diag"),
     RT2_VARIANT(299, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, true); x.fair_prio = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/fair/diag/dpp"),
     // earlier choices of rounds 3-4 (the 5-product form before and after the threshold moved into the accumulator,
     // the first tile forms), kept for A/B; rounds 2-3's 16x16x32 and k16 kernels are in git history
@@ -836,6 +880,7 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     p.mfma_k16_frag = s->d_mfma_k16;
     p.mfma_k16_tau = s->d_mfma_k16_tau;
     p.mfma_k16_bnd = s->d_mfma_k16_bnd;
+    p.mfma_kt_frag = s->d_mfma_kt;
     p.tri_mtl = s->d_mtl;
     p.raw = s->d_raw;
     p.texels = s->d_texels;
@@ -985,6 +1030,7 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
     if (VP && VP->kind == K_RESIDENT && !fits) VP = nullptr;  // cannot hold this scene
     const bool res_fits = (s->n_tris + 31) / 32 <= kResGroups;  // render_mfma_k5r's LDS holds every record group
     if (VP && !res_fits && std::strncmp(VP->name, "mfmar/", 6) == 0) VP = nullptr;
+    if (VP && (s->n_tris + 31) / 32 > kResL2Groups && std::strncmp(VP->name, "mfmarl2/", 8) == 0) VP = nullptr;
     if (VP && (VP->kind == K_MFMA || VP->kind == K_MASSIST) && !s->mfma_ok) VP = nullptr;  // scene outside the filter's range
     // the packed path state (lane_lds = 2) holds 16-bit x, y, rays per pixel and 12-bit bounce counts
     const bool packed = u->width <= 65535 && u->height <= 65535 && u->maxBounceCount <= 4095 &&
@@ -1300,7 +1346,8 @@ extern "C" int rt2_device_selftest(const float* in, int32_t n, float* out10) {
 // Not in rt2.h (test hook): copies one of the scene's derived device arrays to
 // host memory: 0 = pre-transformed triangles (3 float4 each), 1 = render_mfma
 // records (16x16x32 layout), 2 = their per-triangle tau, 3 = sweep_k16 records,
-// 4 = their tau, 5 = the k5 form's per-triangle m.z residual bounds.  Returns the array's size in bytes (nothing copied when
+// 4 = their tau, 5 = the k5 form's per-triangle m.z residual bounds, 6 = the
+// kthr records (threshold in the K-slots).  Returns the array's size in bytes (nothing copied when
 // `host` is null or `bytes` is too small), < 0 on error.
 extern "C" long long rt2_scene_export(rt2_scene* s, int what, void* host, unsigned long long bytes) {
     if (!s) return -1;
@@ -1316,6 +1363,7 @@ extern "C" long long rt2_scene_export(rt2_scene* s, int what, void* host, unsign
     case 3: src = s->d_mfma_k16, sz = n32 * kK16Ops * 16 * sizeof(_Float16); break;
     case 4: src = s->d_mfma_k16_tau, sz = n32 * sizeof(float); break;
     case 5: src = s->d_mfma_k16_bnd, sz = n32 * sizeof(float2); break;
+    case 6: src = s->d_mfma_kt, sz = n32 * kKtOps * 16 * sizeof(_Float16); break;
     default: return -1;
     }
     if (!src || s->n_tris == 0) return 0;
@@ -1333,14 +1381,19 @@ extern "C" long long rt2_scene_export(rt2_scene* s, int what, void* host, unsign
 // 16x16x32 form of render_mfma (variants 150/152), 1 = the k16 form
 // (sweep_k16), 2 = its 5-product form (MfmaSpec::k5: U, -V, X from the first
 // K-half), 3 = the 5-product form with the threshold in the accumulator
-// (MfmaSpec::cthr: U, -V, X, Y shifted by TT = -Tl'', TT in the -tn slot).
+// (MfmaSpec::cthr: U, -V, X, Y shifted by TT = -Tl'', TT in the -tn slot),
+// 4 = layout 3 with the fragments built in registers by frag_pair (the
+// operand path of 282 / 293 / 298), 5 = the threshold in the K-slots
+// (MfmaSpec::kthr, frag_pair fragments: U, -V, X, Y, slot 3 zero).
 // Host outputs, sized by the caller: terms [n_rays][n_pad][5]
-// (n_pad = triangles padded to 16 / 32), frags [n_rays][48] f16 bits, rinfo
-// [n_rays][8], accept [n_rays][n_tris].
+// (n_pad = triangles padded to 16 / 32), frags [n_rays][80] f16 bits (the LDS
+// row of layouts 0..3: main slots 0..31 and Y slots 16..31; layouts 4, 5 also
+// the register fragments the MFMA read: main K-half at 48..63, Y at 64..79),
+// rinfo [n_rays][8], accept [n_rays][n_tris].
 extern "C" int rt2_mfma_probe(rt2_scene* s, int layout, const float* rays, int32_t n_rays, float* terms,
                               uint16_t* frags, float* rinfo, uint8_t* accept) {
     if (!s || !rays || n_rays <= 0 || n_rays % 64 != 0 || !terms || !frags || !rinfo || !accept ||
-        layout < 0 || layout > 3 || s->n_tris < 1 || !s->mfma_ok) {
+        layout < 0 || layout > 5 || s->n_tris < 1 || !s->mfma_ok) {
         rt2h::set_error("rt2_mfma_probe: bad argument (n_rays a positive multiple of 64, a scene in the filter's "
                         "range)");
         return -1;
@@ -1350,7 +1403,7 @@ extern "C" int rt2_mfma_probe(rt2_scene* s, int layout, const float* rays, int32
     const int n_pad = layout >= 1 ? (s->n_tris + 31) / 32 * 32 : (s->n_tris + 15) / 16 * 16;
     const size_t nr = (size_t)n_rays;
     const size_t b_rays = nr * 8 * sizeof(float), b_terms = nr * n_pad * 5 * sizeof(float),
-                 b_frags = nr * 48 * sizeof(uint16_t), b_info = nr * 8 * sizeof(float), b_acc = nr * s->n_tris;
+                 b_frags = nr * 80 * sizeof(uint16_t), b_info = nr * 8 * sizeof(float), b_acc = nr * s->n_tris;
     char* d = nullptr;
     HIPCHECK(hipMalloc(&d, b_rays + b_terms + b_frags + b_info + b_acc + 64));
     char* p0 = d;
@@ -1373,6 +1426,7 @@ extern "C" int rt2_mfma_probe(rt2_scene* s, int layout, const float* rays, int32
         p.mfma_k16_frag = s->d_mfma_k16;
         p.mfma_k16_tau = s->d_mfma_k16_tau;
         p.mfma_k16_bnd = s->d_mfma_k16_bnd;
+        p.mfma_kt_frag = s->d_mfma_kt;
         constexpr MfmaSpec k16 = k16_spec(3), f16x32 = kMfmaT8Y4;
         constexpr MfmaSpec k5 = [] {
             MfmaSpec x = k16_spec(3);
@@ -1386,7 +1440,25 @@ extern "C" int rt2_mfma_probe(rt2_scene* s, int layout, const float* rays, int32
             x.cthr = true;
             return x;
         }();
-        if (layout == 3)
+        // the shipping operand path: fragments by frag_pair (v_permlane32_swap), cthr (282 / 293 / 298) or
+        // kthr (the threshold in the K-slots)
+        constexpr MfmaSpec k5cp = [] {
+            MfmaSpec x = k5_res_spec(4);
+            x.perm_frag = true;
+            return x;
+        }();
+        constexpr MfmaSpec ktp = [] {
+            MfmaSpec x = kt_res_spec(1);
+            x.perm_frag = true;
+            return x;
+        }();
+        if (layout == 4)
+            hipLaunchKernelGGL(mfma_probe_kernel<k5cp>, dim3(n_rays / 64), dim3(64), 0, 0, p, d_rays, n_pad, d_terms,
+                               d_frags, d_info, d_acc);
+        else if (layout == 5)
+            hipLaunchKernelGGL(mfma_probe_kernel<ktp>, dim3(n_rays / 64), dim3(64), 0, 0, p, d_rays, n_pad, d_terms,
+                               d_frags, d_info, d_acc);
+        else if (layout == 3)
             hipLaunchKernelGGL(mfma_probe_kernel<k5c>, dim3(n_rays / 64), dim3(64), 0, 0, p, d_rays, n_pad, d_terms,
                                d_frags, d_info, d_acc);
         else if (layout == 1)

@@ -69,6 +69,7 @@ struct RenderParams {
     const void* mfma_k16_frag;   // MFMA k16: f16 filter records [32-group][op][lane][8] (sweep_k16)
     const float* mfma_k16_tau;   // MFMA k16: per-triangle record scale
     const float2* mfma_k16_bnd;  // MFMA k16: per-triangle bounds of the m.z residual slots (k5 form)
+    const void* mfma_kt_frag;    // MFMA kthr: f16 records [32-group][4 ops][lane][8], threshold in the K-slots
     unsigned long long* wave_log;  // nullable diagnostic: per wave {start, pool dry, end, segments} (ASSIST)
     uint32_t wave_log_n;           // waves the log holds
 };

@@ -590,7 +590,8 @@ class Scene:
     def export(self, what: int, dtype) -> np.ndarray:
         """A derived device array of the scene (rt2_scene_export, test hook): 0 =
         pre-transformed triangles, 1/2 = render_mfma records/tau, 3/4 = sweep_k16 records/tau,
-        5 = the k5 form's per-triangle m.z residual bounds (float32 pairs)."""
+        5 = the k5 form's per-triangle m.z residual bounds (float32 pairs), 6 = the kthr records (threshold in
+        the K-slots)."""
         n = lib().rt2_scene_export(self._p, what, None, 0)
         if n < 0:
             raise RT2Error("rt2_scene_export: bad argument")
@@ -603,19 +604,23 @@ class Scene:
         """The matrix filter's terms on the device (rt2_mfma_probe, test hook):
         rays (n, 8) float32 {o, best, d, 0}, n a multiple of 64; layout 0 =
         16x16x32 (render_mfma), 1 = k16, 2 = its 5-product form (k5), 3 = k5 with the threshold in the
-        accumulator (cthr: U, -V, X, Y shifted by TT, TT in slot 3).  Returns (terms [n, n_pad, 5], frags
-        [n, 48] float16, rinfo [n, 8], accept [n, n_tris] bool)."""
+        accumulator (cthr: U, -V, X, Y shifted by TT, TT in slot 3), 4 = layout 3 with the fragments built in
+        registers (frag_pair: the operand path of the shipping kernels), 5 = the threshold in the K-slots (kthr:
+        U, -V, X, Y; slot 3 zero; frag_pair fragments).  Returns (terms [n, n_pad, 5], frags [n, 48] float16
+        (layouts 4, 5: [n, 80], the register fragments at 48..63 and 64..79), rinfo [n, 8], accept [n, n_tris]
+        bool)."""
         rays = np.ascontiguousarray(rays, dtype=np.float32)
         n = rays.shape[0]
         g = 32 if layout >= 1 else 16
         n_pad = -(-self.n_tris // g) * g
         terms = np.zeros((n, n_pad, 5), dtype=np.float32)
-        frags = np.zeros((n, 48), dtype=np.uint16)
+        frags = np.zeros((n, 80), dtype=np.uint16)
         rinfo = np.zeros((n, 8), dtype=np.float32)
         acc = np.zeros((n, self.n_tris), dtype=np.uint8)
         _check(lib().rt2_mfma_probe(self._p, layout, rays.ctypes.data, n, terms.ctypes.data, frags.ctypes.data,
                                     rinfo.ctypes.data, acc.ctypes.data), "rt2_mfma_probe")
-        return terms, frags.view(np.float16), rinfo, acc.astype(bool)
+        frags = frags.view(np.float16)
+        return terms, (frags if layout >= 4 else np.ascontiguousarray(frags[:, :48])), rinfo, acc.astype(bool)
 
     def stats(self, reset: bool = False) -> Stats:
         s = Stats()

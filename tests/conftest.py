@@ -75,4 +75,8 @@ def require_variant(rt2mod, v):
     """Skips the calling test when kernel variant v is not in the loaded build
     (A/B experiment variants: make EXPERIMENTS=1, RT2_LIB=exp)."""
     if not rt2mod.has_variant(v):
+        # the experiment build carries every listed variant: one missing there
+        # is a lost kernel, not a skip (ADVICE r5)
+        if EXPERIMENTS:
+            pytest.fail(f"variant {v} is listed but missing from the experiment build")
         pytest.skip(f"variant {v} is an experiment variant (not in the product build)")

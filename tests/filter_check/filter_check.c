@@ -283,11 +283,36 @@ static int pass_mfma(f3 o, f3 d, double slot[MQ][32], double tau, float As, floa
         for (int q = 0; q < 3; q++) ch = fmaxf(ch, (float)fabs(slot[q][16])), cl = fmaxf(cl, (float)fabs(slot[q][17]));
         Tl += (ch * (float)fabs(ray[16]) + cl * (float)fabs(ray[17])) * 1.0009765625f;
     }
+    /* k5 = 4 (MfmaSpec::kthr, the threshold in the K-slots): U, -V, X keep
+     * slots 0..12 and 15 (d, m.x, the hi x hi products of m.y and m.z); the
+     * cross slots 13, 14 (m.y) and 16, 17 (m.z) are left out, and two slots
+     * carry -tau x Tw' and -B_q x W': Tw' = Tw (1 + 2^-8) and W' = W (1 + 2^-8)
+     * rounded up to f16, W = mw_y + mw_z with mw_c = max(|ray hi|, 2^11 |ray
+     * lo|) (this ray's own: the smallest a wave's maximum can be), B_q =
+     * 2^-10 max over y, z of max(|coef hi|, 2^11 |coef lo|) rounded up.  Y
+     * carries -tau x Tw' (slot 29).  Each term is its 16 products moved by
+     * 31 u sum|p| toward rejection and passes iff negative. */
+    double kt_thr[3] = {0.0, 0.0, 0.0}, kt_y = 0.0;
+    if (k5 == 4) {
+        const float pad = 1.00390625f;
+        const double tw = f16_up(Tw * pad);
+        const float W = fmaxf((float)fabs(ray[12]), 2048.0f * (float)fabs(ray[13])) +
+                        fmaxf((float)fabs(ray[15]), 2048.0f * (float)fabs(ray[16]));
+        const double w16 = f16_up(W * pad);
+        for (int q = 0; q < 3; q++) {
+            const float ct = fmaxf(fmaxf((float)fabs(slot[q][12]), 2048.0f * (float)fabs(slot[q][14])),
+                                   fmaxf((float)fabs(slot[q][15]), 2048.0f * (float)fabs(slot[q][17])));
+            kt_thr[q] = -(tau * tw + f16_up(ct * 0x1p-10f) * w16);
+        }
+        kt_y = -tau * tw;
+    }
     const float cd = (float)tau * Cw;
     float qv[MQ], qe[MQ];
     for (int q = 0; q < MQ; q++) {
         double s = q == 4 ? cd : TT, sa = q == 4 ? fabs(cd) : fabs(TT);
+        if (k5 == 4 && q < 3) s = kt_thr[q], sa = fabs(kt_thr[q]);
         for (int k = 0; k < 32; k++) {
+            if (k5 == 4 && q < 3 && (k == 13 || k == 14)) continue;  /* kthr: m.y's cross slots left out too */
             if (k5 && q < 3 && (k == 16 || k == 17)) continue;  /* the products the 5-product form leaves out */
             const double p = ray[k] * slot[q][k];
             s += p;
@@ -313,7 +338,7 @@ static int pass_mfma(f3 o, f3 d, double slot[MQ][32], double tau, float As, floa
             yr[18 + 3 * c] = hi, yr[19 + 3 * c] = lo, yr[20 + 3 * c] = hi;
         }
         yr[27] = yr[28] = fin ? -sigma : 0.0f;
-        double sy = TT, sa = fabs(TT);
+        double sy = k5 == 4 ? kt_y : TT, sa = k5 == 4 ? fabs(kt_y) : fabs(TT);
         for (int k = 0; k < 29; k++) {  /* slots 29..31 (the cthr threshold) are 0 in this fragment */
             const double p = yr[k] * slot[3][k];
             sy += p;
@@ -324,7 +349,7 @@ static int pass_mfma(f3 o, f3 d, double slot[MQ][32], double tau, float As, floa
         const float bk = bestK <= Bmax ? bestK : INFINITY;
         Y = fmaf(bk, qv[4] + qe[4], -(qv[3] - qe[3]));
     }
-    if (k5 == 2)  /* no -tn term; all four shifted terms negative */
+    if (k5 == 2 || k5 == 4)  /* no -tn term; all four shifted terms negative */
         return qv[0] + qe[0] < 0.0f && qv[1] + qe[1] < 0.0f && qv[2] + qe[2] < 0.0f && Y < 0.0f;
     /* k5 = 3: the 5-product form without its -tn term (MfmaSpec::no_tn) */
     const float tn = k5 == 3 ? -INFINITY : qv[3] + qe[3];
@@ -339,6 +364,7 @@ int main(int argc, char** argv) {
     long long bad_mfma = 0, p_mfma = 0, n_mfma = 0, p_mfma_near = 0, n_mfma_near = 0;
     long long bad_y = 0, p_y = 0, p_y_near = 0;
     long long bad_k5 = 0, p_k5 = 0, p_k5_near = 0, bad_ct = 0, p_ct = 0, p_ct_near = 0, p_kn = 0, p_kn_near = 0;
+    long long bad_kt = 0, p_kt = 0, p_kt_near = 0;
     for (long long it = 0; it < n; it++) {
         const int kind = (int)(next64() % 6);
         const int far = (next64() % 4) == 0;  /* small triangle far from the origin */
@@ -420,6 +446,10 @@ int main(int argc, char** argv) {
             if (!far && !wide && wk == 0 && inr) p_kn_near += fk;
             p_ct += fc;
             if (ex && !fc) bad_ct++;
+            const int ft = pass_mfma(o, d, slot, tau, As, Ow, Mw, bestK, 1, YMMA_TS, 4);
+            p_kt += ft;
+            if (ex && !ft) bad_kt++;
+            if (!far && !wide && wk == 0 && inr) p_kt_near += ft;
             if (!far && !wide && wk == 0 && inr) p_ct_near += fc;
             n_mfma++;
             p_mfma += fm;
@@ -436,9 +466,11 @@ int main(int argc, char** argv) {
         if (ex && !fo) bad_old++;
         if (ex && !fn) bad_new++;
     }
-    printf("%lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld\n",
+    printf("%lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld"
+           " %lld %lld %lld\n",
            n, accepts, bad_old, bad_new, p_old, p_new, bad_plk, p_plk, bad_mfma, p_mfma, n_mfma, p_mfma_near,
-           n_mfma_near, bad_y, p_y, p_y_near, bad_k5, p_k5, p_k5_near, bad_ct, p_ct, p_ct_near, p_kn, p_kn_near);
+           n_mfma_near, bad_y, p_y, p_y_near, bad_k5, p_k5, p_k5_near, bad_ct, p_ct, p_ct_near, p_kn, p_kn_near,
+           bad_kt, p_kt, p_kt_near);
     fprintf(stderr, "near-origin draws: pass_old %lld pass_plk %lld\n", p_old_near, p_plk_near);
     return 0;
 }

@@ -243,6 +243,99 @@ def analyse_cthr(terms, frags, rinfo, accept, B, tau, T_tau, bnd):
     return out, violations
 
 
+def records_kt(rec, n_tris):
+    """kthr records ([32-group][4 ops][64][8] f16: U, -V, X first K-half, the
+    -tn record's second half) -> slots (n_tris, 4, 16)."""
+    r = rec.view(np.float16).reshape(-1, 4, 2, 32, 8)        # [G, op, k8, t, j]
+    return r.transpose(0, 3, 1, 2, 4).reshape(-1, 4, 16)[:n_tris].astype(np.float64)
+
+
+def perm_fragments_match(frags, live):
+    """Layouts 4 / 5 write the LDS-row slots (0..47) and the fragments the MFMA
+    read after frag_pair (48..79).  For the cthr layout the register main
+    fragment must equal the row's first K-half and the Y fragment the row's Y
+    slots; returns the mismatching (ray, slot) count."""
+    fr = frags[live].astype(np.float32)
+    a = fr[:, 48:64] != fr[:, 0:16]
+    y = fr[:, 64:80] != fr[:, 32:48]
+    return int(a.sum() + y.sum())
+
+
+def kt_expected_fragments(frags, rinfo):
+    """The kthr fragments (kt_frags / kt_y) recomputed on the host from the LDS
+    row slots of the same rays: main K-half = d, m.x (hi lo hi), m.y hi, m.z
+    hi, Tw', W'; Y = the row's Y slots with Tw' at slot 29.  Tw' = f16_up(Tw (1
+    + 2^-8)); W' = f16_up(W (1 + 2^-8)), W = the wave's largest mw_y + mw_z,
+    mw_c = max(|hi|, 2^11 |lo|) (float32 arithmetic as on the device)."""
+    row = frags[:, :48].astype(np.float32)
+    pad = np.float32(1.00390625)
+    tw = f16_up(rinfo[:, 2].astype(np.float32) * pad)
+    mw = (np.maximum(np.abs(row[:, 12]), np.float32(2048.0) * np.abs(row[:, 13])) +
+          np.maximum(np.abs(row[:, 15]), np.float32(2048.0) * np.abs(row[:, 16]))).astype(np.float32)
+    W = np.repeat(mw.reshape(-1, 64).max(1), 64)
+    w16 = f16_up(W * pad)
+    A = np.concatenate([row[:, 0:13], row[:, 15:16], tw[:, None], w16[:, None]], 1).astype(np.float64)
+    Ay = row[:, 32:48].astype(np.float64).copy()
+    Ay[:, 13] = tw
+    return A, Ay, tw, w16
+
+
+def analyse_kt(terms, frags, rinfo, accept, Bkt, B16, T_tau):
+    """One probe run of MfmaSpec::kthr (layout 5).  Checks: the records are the
+    k16 records' slots with the threshold slots as specified (-tau; -B_q =
+    -f16_up(2^-10 max over m.y, m.z of max(|hi|, 2^11 |lo|))); the register
+    fragments the MFMA read equal the host's recomputation; the terms equal
+    the exact sum of their 16 f16 products within the assumed accumulation
+    bound; and every reference-accepted pair has all four terms negative."""
+    n_tris = accept.shape[1]
+    live = rinfo[:, 0] == 1.0
+    tau = T_tau[:n_tris].astype(np.float64)
+    rec_bad = 0
+    for q in range(3):
+        c = B16[:, q, :]
+        ct = np.maximum(np.maximum(np.abs(c[:, 12]), 2048.0 * np.abs(c[:, 14])),
+                        np.maximum(np.abs(c[:, 15]), 2048.0 * np.abs(c[:, 17]))).astype(np.float32)
+        want = np.concatenate([c[:, 0:13], c[:, 15:16], -tau[:, None], -f16_up(ct * np.float32(2.0 ** -10))[:, None]], 1)
+        rec_bad += int((Bkt[:, q, :] != want).sum())
+    want_t = B16[:, 3, 16:32].copy()
+    want_t[:, 13], want_t[:, 14], want_t[:, 15] = -tau, 0.0, 0.0
+    rec_bad += int((Bkt[:, 3, :] != want_t).sum())
+    A_exp, Ay_exp, tw, w16 = kt_expected_fragments(frags, rinfo)
+    fr = frags.astype(np.float64)
+    frag_bad = int((fr[live, 48:64] != A_exp[live]).sum() + (fr[live, 64:80] != Ay_exp[live]).sum())
+    hw = terms[live][:, :n_tris, :].astype(np.float64)
+    A, Ay = fr[live, 48:64], fr[live, 64:80]
+    exact = np.empty(hw.shape[:2] + (4,))
+    sabs = np.empty_like(exact)
+    for q in range(3):
+        exact[..., q] = A @ Bkt[:, q, :].T
+        sabs[..., q] = np.abs(A) @ np.abs(Bkt[:, q, :]).T
+    exact[..., 3] = Ay @ Bkt[:, 3, :].T
+    sabs[..., 3] = np.abs(Ay) @ np.abs(Bkt[:, 3, :]).T
+    sh = hw[..., [0, 1, 2, 4]]
+    acc_err = np.abs(sh - exact)
+    ulp = 2.0 ** -24 * sabs
+    acc_ratio = acc_err / np.where(ulp > 0, ulp, 1.0)
+    passes = (sh.astype(np.float32).view(np.int32) < 0).all(-1)
+    acc = accept[live]
+    violations = np.argwhere(acc & ~passes)
+    # how far the K-slot threshold reaches beyond the base threshold tau Tw
+    base = tau[None, :] * rinfo[live, 2].astype(np.float64)[:, None]
+    grow = (-(A[:, None, 14] * Bkt[None, :, 0, 14]) - A[:, None, 15] * Bkt[None, :, :3, 15].max(-1)) / base
+    out = {
+        "rays_in_range": int(live.sum()), "pairs": int(acc.size), "accepted_pairs": int(acc.sum()),
+        "filter_pass_frac": float(passes.mean()),
+        "record_slot_mismatches": rec_bad,
+        "fragment_slot_mismatches": frag_bad,
+        "acc_err_max_in_2^-24_sum_abs": float(acc_ratio.max()),
+        "acc_err_bound_assumed": 31.0,
+        "threshold_over_tauTw": {"min": float(grow.min()), "mean": float(grow.mean()),
+                                 "p99": float(np.percentile(grow, 99)), "max": float(grow.max())},
+        "violations": int(len(violations)),
+    }
+    return out, violations
+
+
 def _unit(v):
     return v / np.linalg.norm(v, axis=-1, keepdims=True)
 

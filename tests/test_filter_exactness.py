@@ -204,3 +204,40 @@ def test_harness_detects_k5_without_its_bound(tmp_path):
     subprocess.run(["gcc", "-O2", "-std=c11", "-ffp-contract=off", "-o", exe, str(p), "-lm"], check=True)
     (bad, _, _), _ = _run_k5(exe, 1_000_000, 1)
     assert bad > 0
+
+
+def _run_kt(exe, n, seed):
+    """(violations, passes, passes at ordinary scales) of the threshold-in-the-
+    K-slots form (MfmaSpec::kthr) and the same three of the cthr form, on the
+    same draws."""
+    out = subprocess.run([exe, str(n), str(seed)], check=True, capture_output=True, text=True).stdout
+    v = tuple(map(int, out.split()))
+    return v[24:27], v[19:22]
+
+
+@pytest.mark.parametrize("seed", [12, 13])
+def test_matrix_filter_kthr_conservative(checker, seed):
+    """MfmaSpec::kthr: U, -V, X drop the m.y and m.z cross slots, and two
+    k-slots carry -tau Tw' and -B_q W' (the bound of what is dropped); Y
+    carries -tau Tw'.  No accepted pair is skipped, and it passes at most a
+    few percent more pairs than the cthr form (measured: ~1 %)."""
+    (bad, passes, p_near), (bad_c, passes_c, p_near_c) = _run_kt(checker, 2_000_000, seed)
+    assert bad == 0 and bad_c == 0
+    assert passes <= passes_c * 1.03 and p_near <= p_near_c * 1.03
+
+
+@pytest.mark.parametrize("old,new", [
+    # the bound of the dropped m.y / m.z cross products left out of the threshold
+    ("kt_thr[q] = -(tau * tw + f16_up(ct * 0x1p-10f) * w16);", "kt_thr[q] = -(tau * tw + 0.0 * ct * w16);"),
+    # Y without its threshold slot
+    ("kt_y = -tau * tw;", "kt_y = 0.0 * tw;"),
+])
+def test_harness_detects_kthr_without_its_bounds(tmp_path, old, new):
+    src = open(SRC).read()
+    assert old in src
+    p = tmp_path / "mut.c"
+    p.write_text(src.replace(old, new))
+    exe = str(tmp_path / "mut")
+    subprocess.run(["gcc", "-O2", "-std=c11", "-ffp-contract=off", "-o", exe, str(p), "-lm"], check=True)
+    (bad, _, _), _ = _run_kt(exe, 1_000_000, 1)
+    assert bad > 0

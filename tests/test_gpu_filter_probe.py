@@ -131,6 +131,54 @@ def test_filter_cthr_on_hardware(rt2mod, torch_cuda, kind):
     assert st["tt_rel_err_max"] <= 2.0 ** -12, st
 
 
+@pytest.mark.parametrize("kind", KINDS)
+def test_filter_cthr_perm_on_hardware(rt2mod, torch_cuda, kind):
+    """The operand path the shipping cthr kernels (282 / 293 / 298) use: the
+    fragments built in registers by frag_pair (v_permlane32_swap), not read
+    from LDS rows.  The MFMA must see exactly the row's slots, and the layout-3
+    checks (TT, accumulation, conservativeness) must hold on those terms."""
+    rng = np.random.default_rng(200 + KINDS.index(kind))
+    V, rays = fpl.scene_and_rays(kind, rng)
+    scene = rt2mod.Scene(triangles=_tri_array(rt2mod, V), materials=_materials(rt2mod))
+    B = fpl.records_k16(scene.export(3, np.uint16), len(V))
+    T_tau = scene.export(4, np.float32)
+    bnd = fpl.k5_bounds(B)
+    terms, frags, rinfo, accept = scene.mfma_probe(4, rays)
+    live = rinfo[:, 0] == 1.0
+    mism = fpl.perm_fragments_match(frags, live)
+    st, viol = fpl.analyse_cthr(terms, np.ascontiguousarray(frags[:, :48]), rinfo, accept, B, None, T_tau, bnd)
+    st["fragment_slot_mismatches"] = mism
+    _results[f"{kind}/cthr_perm"] = st
+    print(json.dumps(st, indent=1))
+    assert mism == 0
+    assert st["rays_in_range"] >= len(rays) // 2 and st["accepted_pairs"] > 0
+    assert st["violations"] == 0, f"reference-accepted pairs rejected: {viol[:10]}"
+    assert st["tt_over_Tl_min"] > 1.0, st
+    assert st["acc_err_max_in_2^-24_sum_abs"] <= st["acc_err_bound_assumed"], st
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_filter_kthr_on_hardware(rt2mod, torch_cuda, kind):
+    """MfmaSpec::kthr (the threshold in the K-slots) on the hardware, with the
+    shipping frag_pair operand path: the kt records and register fragments are
+    as specified, the terms are their 16 f16 products' exact sum within the
+    assumed accumulation bound, and every reference-accepted pair passes."""
+    rng = np.random.default_rng(300 + KINDS.index(kind))
+    V, rays = fpl.scene_and_rays(kind, rng)
+    scene = rt2mod.Scene(triangles=_tri_array(rt2mod, V), materials=_materials(rt2mod))
+    B16 = fpl.records_k16(scene.export(3, np.uint16), len(V))
+    Bkt = fpl.records_kt(scene.export(6, np.uint16), len(V))
+    T_tau = scene.export(4, np.float32)
+    terms, frags, rinfo, accept = scene.mfma_probe(5, rays)
+    st, viol = fpl.analyse_kt(terms, frags, rinfo, accept, Bkt, B16, T_tau)
+    _results[f"{kind}/kthr"] = st
+    print(json.dumps(st, indent=1))
+    assert st["record_slot_mismatches"] == 0 and st["fragment_slot_mismatches"] == 0, st
+    assert st["rays_in_range"] >= len(rays) // 2 and st["accepted_pairs"] > 0
+    assert st["violations"] == 0, f"reference-accepted pairs rejected by the kthr filter: {viol[:10]}"
+    assert st["acc_err_max_in_2^-24_sum_abs"] <= st["acc_err_bound_assumed"], st
+
+
 def test_write_probe_summary():
     out = os.environ.get("RT2_PROBE_OUT")
     if not out or not _results:
@@ -189,7 +237,8 @@ def near_threshold_scene(rt2mod):
     return sd
 
 
-@pytest.mark.parametrize("variant", [227, 228, 231, 233, 212, 213, 217, 260, 261, 262, 263, 243, 250, 252, 280, 282, 288, 293, 298])
+@pytest.mark.parametrize("variant", [227, 228, 231, 233, 212, 213, 217, 260, 261, 262, 263, 243, 250, 252, 280, 282, 293, 298,
+                                     320, 321, 322, 323, 325])
 def test_near_threshold_scene_bit_exact(rt2mod, oraclemod, torch_cuda, variant):
     if not rt2mod.has_variant(variant):
         pytest.skip(f"variant {variant} not in this build")

@@ -16,7 +16,7 @@ MFMA = 227
 # every matrix-filter variant of the loaded library runs each case: the
 # product build's automatic kernels (227, 262, 263, the LDS-resident 282 and
 # the LDS-tiled 217 / 293); the experiment build adds its A/B variants
-# (other drain thresholds, wave counts, record tiles, tail jobs: 288)
+# (other drain thresholds, wave counts, record tiles, the kthr forms 320-325)
 
 
 def _mfma_variants():

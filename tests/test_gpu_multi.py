@@ -147,6 +147,33 @@ def test_comm_gather_slabs_one_rank(rt2mod, config_scene, torch_cuda):
     comm.close()
 
 
+def test_comm_gather_slabs_after_long_render(rt2mod, config_scene, torch_cuda, monkeypatch):
+    """INTEGRATION.md's async sequence on ONE stream — rt2_render,
+    resolve, rt2_gather_slabs, rt2_comm_wait — with a render many times longer
+    than RT2_COMM_TIMEOUT_S.  rt2_comm_wait waits for the rank's own queued
+    work (everything before the gather) outside the deadline, then applies the
+    deadline to the gather: a healthy job completes, bit-identical."""
+    import time
+    torch = torch_cuda
+    sd, spec = config_scene("B")
+    u = rt2mod.offline_uniforms(1920, 1080, spec.bounces, 64, sd.num_triangles)
+    scene = rt2mod.Scene(sd, 0)
+    ref = scene.render_host(u, 0, 1)
+    comm = rt2mod.Comm(rt2mod.Comm.unique_id(), 1, 0, 0)
+    stream = torch.cuda.current_stream().cuda_stream
+    torch.cuda.synchronize()
+    monkeypatch.setenv("RT2_COMM_TIMEOUT_S", "0.02")
+    t0 = time.time()
+    slab = render_slab(rt2mod, torch, scene, u, 1, rt2mod.shard())  # queued, not waited for
+    image = torch.zeros_like(slab)
+    comm.gather_slabs(slab.data_ptr(), u.width, u.height, rt2mod.shard(), 0, image.data_ptr(), stream)
+    comm.wait(stream)
+    assert time.time() - t0 > 3 * 0.02  # the render alone outlasts the deadline several times
+    comm.check()
+    assert np.array_equal(image.cpu().numpy(), ref)
+    comm.close()
+
+
 @pytest.mark.parametrize("site", ["gather.prepare", "check", "render", "gather.issue", "agree.copy"])
 def test_comm_one_rank_injected_faults(rt2mod, config_scene, torch_cuda, site, monkeypatch):
     """The failure sites of rt2_comm_protocol.h under RCCL (RT2_FAULT_AT): the

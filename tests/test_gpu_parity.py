@@ -402,8 +402,9 @@ def test_frame_split_identical(rt2mod, oraclemod, config_scene, torch_cuda, trav
 # 282/298 = its LDS-resident forms, 136 = the scalar path forced) and, in an experiment build, the A/B
 # variants (masked/plk filters, resident LDS, cooperative and team tail modes,
 # split waves, the round-1 slab kernels, occupancy hints)
-BRUTE_VARIANTS = [0, 86, 92, 217, 227, 262, 263, 282, 293, 298, 136] + ([213, 231, 243, 252, 260, 261, 150, 152, 200, 206, 228, 233, 250, 137, 138, 139, 140, 143, 144, 145, 146] if EXPERIMENTS else []) + ([22, 24, 28, 52, 64, 65, 66, 67, 68, 70, 71, 72, 73, 74, 76, 79, 80, 84, 85, 87, 89, 95, 97, 101, 104, 106,
-                                 90] if EXPERIMENTS else [])
+BRUTE_VARIANTS = [0, 86, 92, 217, 227, 262, 263, 282, 293, 298, 136] + (
+    [213, 231, 243, 252, 260, 261, 212, 246, 228, 233, 250, 280, 320, 321, 322, 323, 325, 67, 85, 106, 64, 66, 74, 76,
+     79, 80] if EXPERIMENTS else [])
 
 
 @pytest.mark.parametrize("variant", BRUTE_VARIANTS)
@@ -421,7 +422,7 @@ def test_brute_variants_bit_exact(rt2mod, oraclemod, config_scene, torch_cuda, v
     assert st.segments == segs
 
 
-@pytest.mark.parametrize("variant", [92] + ([138, 139, 71, 72, 84, 85, 90] if EXPERIMENTS else []))
+@pytest.mark.parametrize("variant", [92] + ([85] if EXPERIMENTS else []))
 @pytest.mark.parametrize("split_frames", [False, True])
 def test_split_waves_outputs(rt2mod, oraclemod, config_scene, torch_cuda, variant, split_frames):
     """Kernels whose waves share rays — split mode (S waves per 64 rays, one
