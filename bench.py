@@ -2,7 +2,7 @@
 """Benchmark of the MI355X render path on BASELINE.json's metric.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config B] [--traversal brute|bvh]
-                    [--no-cpu-baseline] [--no-alt] [--no-config-c] [--no-config-e] [--no-scalar]
+                    [--no-cpu-baseline] [--no-alt] [--no-config-c] [--no-config-e] [--no-config-w] [--no-scalar]
 
 --gpus N > 1 without a launcher starts N ranks itself (torch.distributed.run,
 one process per GPU, master 127.0.0.1); under a launcher WORLD_SIZE must equal N.
@@ -36,6 +36,9 @@ Prints ONE JSON line (rank 0):
                 whether the >= 10x target is met and by which kernel
   config_E      (1 GPU, config B runs) 1M triangles, mirror box, 16 bounces, 4
                 spp: the same legs as config_C
+  config_W      (1 GPU, config B runs) config B with the reference's windmill
+                model (1,821 triangles = 57 groups: beyond the 38 whose records
+                the LDS holds): the same legs
   scalar_valu   (1 GPU) the no-MFMA scalar-path kernel (render_smem) on the
                 headline workload with its FP32-VALU roofline and parity
 """
@@ -68,7 +71,7 @@ MFMA_K5_FLOP_PER_PAIR = 160   # its 5-product form (MfmaSpec::k5): 5 v_mfma_f32_
 MFMA_K5_NOTN_FLOP_PER_PAIR = 128  # ... without the -tn term (small scenes): 4 per 1,024 pairs
 SCALAR_VARIANT = 136       # render_smem forced (rt2_render.hip): the no-MFMA scalar-path kernel
 TARGET_RATIO = 10.0        # north star: >= 10x the CPU reference at config C on 1 GPU
-KERNEL_FILES = {"mfmat5": "render_mfma_k5t", "mfmar": "render_mfma_k5r", "mfma": "render_mfma", "massist": "render_assist", "smem": "render_smem", "split": "render_split", "tiled": "render_tiled", "assist": "render_assist",
+KERNEL_FILES = {"mfmat5": "render_mfma_k5t", "mfmarl2": "render_mfma_k5r", "mfmar": "render_mfma_k5r", "mfma": "render_mfma", "massist": "render_assist", "smem": "render_smem", "split": "render_split", "tiled": "render_tiled", "assist": "render_assist",
                 "resident": "render_resident", "bvh4": "render_bvh4", "bvh3": "render_bvh3", "bvh2": "render_bvh2",
                 "bvh": "render_bvh"}
 
@@ -87,6 +90,8 @@ def parse():
     ap.add_argument("--no-alt", action="store_true", help="skip timing the other traversal beside the headline")
     ap.add_argument("--no-config-c", action="store_true", help="skip the config C (north-star target) leg")
     ap.add_argument("--no-config-e", action="store_true", help="skip the config E (1M triangles, mirror box) leg")
+    ap.add_argument("--no-config-w", action="store_true",
+                    help="skip the config W leg (windmill + Cornell box: 57 triangle groups, beyond the 38 the LDS holds)")
     ap.add_argument("--no-scalar", action="store_true",
                     help="skip the scalar-VALU leg (render_smem, the north star's no-MFMA kernel, on the headline workload)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target seconds per CPU baseline mode")
@@ -218,15 +223,19 @@ def roofline(tests, visits, kern_ms, segments=0, n_tris=0, variant=None):
                                    "frac": round(hbm / HBM_PEAK_GBS, 3),
                                    "note": "36 B x tests; >1 = on-chip reuse (effective bandwidth)"}}
     if variant and variant.startswith(("mfma", "massist")) and segments and n_tris:
-        k5 = "/k5/" in variant
+        kt = re.search(r"/kt\d/", variant) is not None  # the threshold in the K-slots: U, -V, X, Y per block
+        k5 = "/k5/" in variant or kt
         k16 = "/k16/" in variant or k5
         group = 32 if k16 else 16
         pairs = segments * (-(-int(n_tris) // group) * group)
-        notn = k5 and "/notn/" in variant
+        notn = k5 and ("/notn/" in variant or kt)
         fpp = (MFMA_K5_NOTN_FLOP_PER_PAIR if notn else MFMA_K5_FLOP_PER_PAIR if k5 else MFMA_K16_FLOP_PER_PAIR if k16
                else MFMA_FLOP_PER_PAIR)
         mf = fpp * pairs / (kern_ms * 1e-3) / 1e12
-        model = ("128 x (ray, triangle) pairs: the 5-product k16 form without -tn, 4 v_mfma_f32_32x32x16_f16 per "
+        model = ("128 x (ray, triangle) pairs: the threshold in the K-slots, 4 v_mfma_f32_32x32x16_f16 per 32 rays "
+                 "x 32 triangles (U, -V, X, Y: one K-half each, the threshold two of its slots), triangles padded to 32"
+                 if kt else
+                 "128 x (ray, triangle) pairs: the 5-product k16 form without -tn, 4 v_mfma_f32_32x32x16_f16 per "
                  "32 rays x 32 triangles (U, -V, X, Y: one K-half each), triangles padded to 32" if notn else
                  "160 x (ray, triangle) pairs: the 5-product k16 form's 5 v_mfma_f32_32x32x16_f16 per 32 rays x 32 "
                  "triangles (U, -V, X, -tn, Y: one K-half each), triangles padded to 32" if k5 else
@@ -411,7 +420,7 @@ def config_leg(torch, rt2, stream, threads, host, seconds, do_cpu, name="C"):
            "rays_per_pixel": spec.rays, "frames": spec.frames, "max_bounce": spec.bounces,
            "triangles": sd.num_triangles}
     legs, imgs = {}, {}
-    for trav, steps, warm in (("bvh", 3, 1), ("brute", 1, 0)):
+    for trav, steps, warm in (("bvh", 3, 1), ("brute", 1 if sd.num_triangles > 20000 else 3, 0 if sd.num_triangles > 20000 else 1)):
         progress(f"config {name}: {trav} ({steps} step(s))")
         scene.set_traversal(trav)
         for _ in range(warm):
@@ -647,10 +656,10 @@ def main():
                 f"reference BVH traversal (compute.glsl:410-460), {res['bvh']['seconds']:.1f} s")
         out["cpu_baseline"] = cpu_summary(res, threads, host, desc, gpu_values)
         out["parity"] = parity
-    if world == 1 and spec.name == "B" and not (args.no_config_c and args.no_config_e):
+    if world == 1 and spec.name == "B" and not (args.no_config_c and args.no_config_e and args.no_config_w):
         scene.close()
         torch.cuda.empty_cache()
-        for name, skip in (("C", args.no_config_c), ("E", args.no_config_e)):
+        for name, skip in (("C", args.no_config_c), ("E", args.no_config_e), ("W", args.no_config_w)):
             if not skip:
                 progress(f"config {name} leg")
                 out[f"config_{name}"] = config_leg(torch, rt2, stream, threads, host, args.cpu_seconds,

@@ -128,12 +128,26 @@ __device__ __forceinline__ bool sweep_kt_res(const RenderParams& p, const h8* re
     const int nres = S.res_l2 ? min(ng, S.res_groups) : ng;
     cfloat* const tri = (cfloat*)p.tri;
     const h8* tb = rec + lane;
-    for (int G = 0; G < nres; G++) {
-        const h8 b0 = tb[0], b1 = tb[64], b2 = tb[128], b3 = tb[192];
-        tb += kKtOps * 64;
-        const unsigned long long M = kt_group<S>(a0, y1, b0, b1, b2, b3, upper);
-        if constexpr (S.diag) dg.groups += 1;
-        if (M && exact_group<S>(M, G, n_tris, tri, o, d, best, bi, bestK, dg)) kt_y(d, o, bestK, sc, tw16, y1);
+    if constexpr (S.prefetch) {
+        // MfmaSpec::prefetch: the next group's operands are read from LDS
+        // while this group's products run (a second register set)
+        h8 n0 = tb[0], n1 = tb[64], n2 = tb[128], n3 = tb[192];
+        for (int G = 0; G < nres; G++) {
+            const h8 b0 = n0, b1 = n1, b2 = n2, b3 = n3;
+            tb += kKtOps * 64;
+            if (G + 1 < nres) n0 = tb[0], n1 = tb[64], n2 = tb[128], n3 = tb[192];
+            const unsigned long long M = kt_group<S>(a0, y1, b0, b1, b2, b3, upper);
+            if constexpr (S.diag) dg.groups += 1;
+            if (M && exact_group<S>(M, G, n_tris, tri, o, d, best, bi, bestK, dg)) kt_y(d, o, bestK, sc, tw16, y1);
+        }
+    } else {
+        for (int G = 0; G < nres; G++) {
+            const h8 b0 = tb[0], b1 = tb[64], b2 = tb[128], b3 = tb[192];
+            tb += kKtOps * 64;
+            const unsigned long long M = kt_group<S>(a0, y1, b0, b1, b2, b3, upper);
+            if constexpr (S.diag) dg.groups += 1;
+            if (M && exact_group<S>(M, G, n_tris, tri, o, d, best, bi, bestK, dg)) kt_y(d, o, bestK, sc, tw16, y1);
+        }
     }
     if constexpr (S.res_l2) {
         const h8* gb = reinterpret_cast<const h8*>(p.mfma_kt_frag) + (size_t)nres * (kKtOps * 64) + lane;

@@ -709,6 +709,11 @@ const Variant kVariants[] = {
     RT2_VARIANT(323, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = kt_res_spec(1); x.fair_prio = true; return x; }()>, 1024, "mfmar/1024/kt1/res38/coop4/w4/cmp/fair/dpp"),
     RT2_VARIANT(324, K_MFMA, render_mfma_k5r<kt_res_spec(1, true)>, 1024, "mfmar/1024/kt1/res38/coop4/w4/cmp/diag/dpp"),
     RT2_VARIANT(325, K_MFMA, render_mfma_k5r<kt_res_spec(1, false, true)>, 1024, "mfmarl2/1024/kt1/res38l2/coop4/w4/cmp/dpp"),
+    // ... at 3 waves per SIMD (168 VGPRs: the four products before the reduction fit), with the next group's
+    // operands read ahead
+    RT2_VARIANT(326, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = kt_res_spec(1); x.block = 768; x.waves = 3; return x; }()>, 768, "mfmar/768/kt1/res38/coop4/w3/cmp/dpp"),
+    RT2_VARIANT(327, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = kt_res_spec(1); x.block = 768; x.waves = 3; x.prefetch = true; return x; }()>, 768, "mfmar/768/kt1/res38/coop4/w3/cmp/dpp/pf"),
+    RT2_VARIANT(328, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = kt_res_spec(1); x.prefetch = true; return x; }()>, 1024, "mfmar/1024/kt1/res38/coop4/w4/cmp/dpp/pf"),
     // ... on the LDS-tiled kernel (the form of 293): 19-group tiles at 3 waves per SIMD (schedules 1, 2), 16-group
     // tiles at 4 waves
     RT2_VARIANT(330, K_MFMA, render_mfma_k5t<kt_tiles_spec(19, 3, 1)>, 768, "mfmat5/768/kt1/tile19/coop0/w3/cmp/regs/perm"),

@@ -5,8 +5,8 @@ SURVEY.md §8e: every (pixel, frame) is independent and its seed depends only on
 interleaved in tiles of `tile_rows` (rank r owns tiles t = r, r+N, ...) for load
 balance (the cost of an image region depends on what it shows).  Each rank
 renders its slab into a device accumulator, resolves it, and the slabs are
-gathered to rank 0 with ONE collective (RCCL all_gather_into_tensor over xGMI
-when the backend is "nccl"); rank 0 un-interleaves.  The result is
+gathered to rank 0 with ONE collective (torch.distributed.gather: RCCL's gather
+over xGMI when the backend is "nccl"); rank 0 un-interleaves.  The result is
 bit-identical to a single-GPU render (same per-pixel arithmetic).
 
 The per-rank slab renderer is injectable so the sharding/gather logic can be

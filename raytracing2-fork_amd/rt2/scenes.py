@@ -5,13 +5,20 @@ B  campfire + addCornellBox(0.17, 0.3, light, true)                  1,208,     
 C  torus 250x200 quads (100k tris) + addCornellBox                   100,016,   1920x1080, R64 F4  B8
 D  scene B                                                           1,208,     3840x2160, R64 F16 B8
 E  torus 1000x500 (1M tris) + addMirrorCornellBox                    1,000,014, 1920x1080, R4  F1  B16
+W  windmill + addCornellBox(0.17, 0.3, light, true)                  1,821,     1920x1080, R64 F1  B8
+K  cat + addCornellBox(0.17, 0.3, light, true)                       2,848,     1920x1080, R64 F1  B8
+
+W and K (not in SURVEY.md §8d) are config B with two of
+the reference's other texture-free bundled models: scenes of 57 and 89
+32-triangle groups, beyond the 38 whose records the LDS holds.
 
 Camera = reference defaults (rayTracing.cpp:82-89), environmental light on,
 seed schedule x + y*W + frame*968824447 (compute.glsl:668).
 
-The campfire model is taken from the reference's RayTracing/Data/campfire when
-that tree is present (here), else from the loader-output fixture
-tests/golden/campfire_loaded.npz (the GPU box has no reference tree); the
+The campfire (windmill, cat) model is taken from the reference's
+RayTracing/Data/<model> when that tree is present (here), else from the
+loader-output fixture tests/golden/<model>_loaded.npz (the GPU box has no
+reference tree); the
 torus OBJ is generated deterministically and goes through the same loader.
 """
 from __future__ import annotations
@@ -26,6 +33,7 @@ import numpy as np
 REF_DATA_ENV = "RT2_REFERENCE_DATA"
 _REPO = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", ".."))
 CAMPFIRE_FIXTURE = os.path.join(_REPO, "tests", "golden", "campfire_loaded.npz")
+MODEL_OF = {"B": "campfire", "D": "campfire", "W": "windmill", "K": "cat"}
 
 
 @dataclass(frozen=True)
@@ -45,6 +53,8 @@ CONFIGS = {
     "C": ConfigSpec("C", 1920, 1080, 64, 4, 8, "torus 250x200 quads (100,000 tris) + addCornellBox, 100,016 tris"),
     "D": ConfigSpec("D", 3840, 2160, 64, 16, 8, "scene B at 4K, 1024 spp"),
     "E": ConfigSpec("E", 1920, 1080, 4, 1, 16, "torus 1000x500 quads (1,000,000 tris) + addMirrorCornellBox"),
+    "W": ConfigSpec("W", 1920, 1080, 64, 1, 8, "windmill (1,805 tris) + addCornellBox, 1,821 tris"),
+    "K": ConfigSpec("K", 1920, 1080, 64, 1, 8, "cat (2,832 tris) + addCornellBox, 2,848 tris"),
 }
 
 
@@ -98,14 +108,15 @@ def _append_main_materials(sd, Material):
     return red, green, wall, light, mirror
 
 
-def _load_campfire(sd) -> None:
+def _load_model(sd, model: str = "campfire") -> None:
     d = reference_data_dir()
-    if d and os.path.isdir(os.path.join(d, "campfire")):
-        sd.load_obj_folder(os.path.join(d, "campfire"))
+    if d and os.path.isdir(os.path.join(d, model)):
+        sd.load_obj_folder(os.path.join(d, model))
         return
-    if not os.path.exists(CAMPFIRE_FIXTURE):
-        raise FileNotFoundError("neither the reference campfire model nor " + CAMPFIRE_FIXTURE)
-    z = np.load(CAMPFIRE_FIXTURE, allow_pickle=False)
+    fixture = os.path.join(_REPO, "tests", "golden", f"{model}_loaded.npz")
+    if not os.path.exists(fixture):
+        raise FileNotFoundError(f"neither the reference {model} model nor " + fixture)
+    z = np.load(fixture, allow_pickle=False)
     from . import Material
     import ctypes as C
     for m in z["materials"]:
@@ -123,8 +134,8 @@ def build_config_scene(name: str, workdir: str | None = None):
     if spec.name == "A":
         red, green, wall, light, mirror = _append_main_materials(sd, Material)
         sd.create_classic_cornell_box(10.0, red, green, wall, light)
-    elif spec.name in ("B", "D"):
-        _load_campfire(sd)
+    elif spec.name in ("B", "D", "W", "K"):
+        _load_model(sd, MODEL_OF[spec.name])
         red, green, wall, light, mirror = _append_main_materials(sd, Material)
         sd.add_cornell_box(0.17, 0.3, light, True)
     elif spec.name in ("C", "E"):

@@ -61,7 +61,7 @@ for c in ${STATS}; do
     *) a="--config $c --steps 1 --warmup 0" ;;
   esac
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/stats_${T}_$c" -o run -- \
-    python3 bench.py --no-cpu-baseline --no-config-c --no-config-e --no-scalar --no-alt $a > "gpurun_out/stats_${T}_$c.log" 2>&1 \
+    python3 bench.py --no-cpu-baseline --no-config-c --no-config-e --no-config-w --no-scalar --no-alt $a > "gpurun_out/stats_${T}_$c.log" 2>&1 \
     || { echo "stats $c failed"; tail -20 "gpurun_out/stats_${T}_$c.log"; exit 1; }
   echo "stats $c ok"
 done

@@ -4,7 +4,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-ARGS="--no-cpu-baseline --no-alt --no-config-c --no-config-e --no-scalar --steps 2 --warmup 1 ${BENCH_ARGS}"
+ARGS="--no-cpu-baseline --no-alt --no-config-c --no-config-e --no-config-w --no-scalar --steps 2 --warmup 1 ${BENCH_ARGS}"
 OUTD="$GRAFT_REPO_ROOT/${PMC_OUT:-gpurun_out}"
 mkdir -p "$OUTD"
 run() {

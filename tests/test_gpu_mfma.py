@@ -48,13 +48,17 @@ def torch_cuda():
 
 
 RES_MAX_TRIS = 38 * 32  # render_mfma_k5r ("mfmar"): records resident in LDS, scenes of <= 38 groups
+RESL2_MAX_TRIS = 256 * 32  # ... "mfmarl2": 38 groups resident, the rest from L2, scenes of <= 256 groups
 
 
 def mfma_scene(rt2mod, sd=None, variant=MFMA, **kw):
     require_variant(rt2mod, variant)
     n = sd.num_triangles if sd is not None else len(kw["triangles"])
-    if rt2mod.lib().rt2_variant_name(variant).decode().startswith("mfmar/") and n > RES_MAX_TRIS:
+    name = rt2mod.lib().rt2_variant_name(variant).decode()
+    if name.startswith("mfmar/") and n > RES_MAX_TRIS:
         pytest.skip(f"variant {variant} holds scenes of <= {RES_MAX_TRIS} triangles")
+    if name.startswith("mfmarl2/") and n > RESL2_MAX_TRIS:
+        pytest.skip(f"variant {variant} holds scenes of <= {RESL2_MAX_TRIS} triangles")
     scene = rt2mod.Scene(sd, 0) if sd is not None else rt2mod.Scene(**kw)
     scene.set_variant(variant)
     return scene
@@ -88,6 +92,20 @@ def test_config_C_small_image(rt2mod, oraclemod, config_scene, torch_cuda, mfma_
     img = scene.render_host(u, 0, 1)
     ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(27), 0, 1)
     assert_exact(img, ref, "mfma config C")
+
+
+@pytest.mark.parametrize("cfg", ["W", "K"])
+def test_mid_size_models(rt2mod, oraclemod, config_scene, torch_cuda, mfma_variant, cfg):
+    """Configs W and K (windmill, cat + the Cornell box: 57 and 89 groups,
+    beyond the 38 the LDS holds): every variant that can hold them, the L2
+    continuation of the resident kernel (mfmarl2) included, bit-exact on a
+    small whole image."""
+    sd, spec = config_scene(cfg)
+    u = rt2mod.offline_uniforms(64, 36, spec.bounces, 4, sd.num_triangles)
+    scene = mfma_scene(rt2mod, sd, mfma_variant)
+    img = scene.render_host(u, 0, 1)
+    ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(36), 0, 1)
+    assert_exact(img, ref, f"config {cfg}")
 
 
 def test_diverse_materials(rt2mod, oraclemod, torch_cuda, mfma_variant):

@@ -328,8 +328,9 @@ def test_defocus_and_frame_wrap(rt2mod, oraclemod, config_scene, torch_cuda):
 
 
 def test_tiled_kernel_exact(rt2mod, oraclemod, config_scene, torch_cuda):
-    """The LDS-tiled sweep (the automatic choice above 131,072 triangles), forced
-    on config B and on config C's 100k triangles."""
+    """The scalar-path LDS-tiled sweep (variant 86: the automatic choice above
+    131,072 triangles for scenes outside the matrix filter's range), forced on
+    config B and on config C's 100k triangles."""
     sd, spec = config_scene("B")
     u = rt2mod.offline_uniforms(96, 54, 8, 4, sd.num_triangles)
     scene = rt2mod.Scene(sd, 0)
@@ -343,7 +344,7 @@ def test_tiled_kernel_exact(rt2mod, oraclemod, config_scene, torch_cuda):
     u = rt2mod.offline_uniforms(24, 14, 8, 2, sdc.num_triangles)
     ref, _, _ = oracle_mean(oraclemod, sdc, u, np.arange(14), 0, 1, "bvh")
     out = {}
-    for v in (86, 0):  # forced LDS tiles; automatic (the scalar path at 100k triangles)
+    for v in (86, 0):  # forced scalar-path LDS tiles; automatic (the matrix filter's tiled kernel at 100k triangles)
         scene = rt2mod.Scene(sdc, 0)
         scene.set_variant(v)
         out[v] = scene.render_host(u, 0, 1)

@@ -48,9 +48,13 @@ def test_campfire_counts_and_lights(rt2mod):
 
 
 @needs_reference
-def test_campfire_fixture_matches_loader(rt2mod):
-    sd = load(rt2mod, os.path.join(DATA, "campfire"))
-    z = np.load(os.path.join(GOLDEN, "campfire_loaded.npz"), allow_pickle=False)
+@pytest.mark.parametrize("model", ["campfire", "windmill", "cat"])
+def test_model_fixture_matches_loader(rt2mod, model):
+    """The loader-output fixtures the GPU box builds configs B/D, W and K from
+    (tests/golden/make_golden.py, make_models.py) equal the loader's output on
+    the reference's model files."""
+    sd = load(rt2mod, os.path.join(DATA, model))
+    z = np.load(os.path.join(GOLDEN, f"{model}_loaded.npz"), allow_pickle=False)
     assert sd.triangles().tobytes() == z["triangles"].tobytes()
     assert sd.materials().tobytes() == z["materials"].tobytes()
 
