@@ -266,7 +266,11 @@ int rt2_gather_slabs(rt2_comm* comm, const void* d_slab, int32_t width, int32_t 
  * RT2_COMM_TIMEOUT_S deadline, polling ncclCommGetAsyncError: 0 when it has
  * drained; on a timeout, an RCCL error or a stream error the communicator is
  * aborted as above and < 0 returned (replaces the caller's
- * hipStreamSynchronize / cudaStreamSynchronize after the collective). */
+ * hipStreamSynchronize / cudaStreamSynchronize after the collective).  When
+ * the last rt2_gather_slabs of this communicator was queued on `stream`, the
+ * work queued before that gather (this rank's render: no peer is involved) is
+ * waited for first, outside the deadline (bounded at 20 x the timeout), and
+ * twice its duration is added to the deadline of the gather itself. */
 int rt2_comm_wait(rt2_comm* comm, void* stream);
 /* The root's un-interleave alone: d_gathered = [nranks][max_rows][width]
  * 16-byte pixels (rank-major slabs, padded to max_rows rows) -> d_image

@@ -898,9 +898,57 @@ __device__ __forceinline__ void kt_y(const f3& d, const f3& o, float bkv, const 
 template <MfmaSpec S>
 __device__ __forceinline__ unsigned long long kt_group(const h8* a0, const h8* y1, const h8& bu, const h8& bv,
                                                        const h8& bx, const h8& bt, bool upper) {
-    static_assert(S.kthr >= 1 && S.kthr <= 3, "kthr schedule");
+    static_assert(S.kthr >= 1 && S.kthr <= 4, "kthr schedule");
     const f16v zero = {};
     int acc = 0;
+    if constexpr (S.kthr == 4) {
+        // kthr 4: the two blocks interleaved so that each wave's own products
+        // run beside its own reduction VALU, at cthr's register peak (48
+        // product VGPRs): [U0 V0 X0] [AND0] [Y0 U1] [fold0] [V1 X1] [AND1]
+        // [Y1] [fold1] (scheduling groups; one basic block per form)
+        auto andv = [](const f16v& U, const f16v& V, const f16v& X, int* t3) {
+#pragma unroll
+            for (int i = 0; i < 16; i++)
+                t3[i] = __builtin_amdgcn_bitop3_b32(__float_as_int(U[i]), __float_as_int(V[i]), __float_as_int(X[i]), 0x80);
+        };
+        auto fold = [](const int* t3, const f16v& Y, int a) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) a = __builtin_amdgcn_bitop3_b32(t3[i], __float_as_int(Y[i]), a, 0xEA);
+            return a;
+        };
+        if (upper) {
+            int t0[16], t1[16];
+            const f16v U0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[0], bu, zero, 0, 0, 0);
+            const f16v V0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[0], bv, zero, 0, 0, 0);
+            const f16v X0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[0], bx, zero, 0, 0, 0);
+            andv(U0, V0, X0, t0);
+            const f16v Y0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(y1[0], bt, zero, 0, 0, 0);
+            const f16v U1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[1], bu, zero, 0, 0, 0);
+            acc = fold(t0, Y0, acc);
+            const f16v V1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[1], bv, zero, 0, 0, 0);
+            const f16v X1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[1], bx, zero, 0, 0, 0);
+            andv(U1, V1, X1, t1);
+            const f16v Y1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(y1[1], bt, zero, 0, 0, 0);
+            acc = fold(t1, Y1, acc);
+            __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
+        } else {
+            int t0[16];
+            const f16v U0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[0], bu, zero, 0, 0, 0);
+            const f16v V0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[0], bv, zero, 0, 0, 0);
+            const f16v X0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[0], bx, zero, 0, 0, 0);
+            andv(U0, V0, X0, t0);
+            const f16v Y0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(y1[0], bt, zero, 0, 0, 0);
+            acc = fold(t0, Y0, acc);
+        }
+        return __ballot(acc < 0);
+    }
 #pragma unroll
     for (int R = 0; R < 2; R++) {
         if (R == 1 && !upper) break;

@@ -82,8 +82,11 @@ __device__ __forceinline__ void advance(Lane& L, const RenderParams& p) {
                     L.item = it32 - f * np32;
                     if (p.order && L.item < p.n_runs * 64u) L.item = p.order[L.item >> 6] * 64u + (L.item & 63u);
                     // cost map (opt-in): the item's start clock waits in its own
-                    // slot (no register of the lane carries it)
-                    if (p.cost_out && split_writer<S>()) p.cost_out[L.item] = (uint32_t)__builtin_amdgcn_s_memtime();
+                    // slot (no register of the lane carries it); with frame-major
+                    // items only frame 0 of a pixel measures (one writer per
+                    // slot: the pixel's other frames run at the same time)
+                    if (p.cost_out && split_writer<S>() && f == 0u)
+                        p.cost_out[L.item] = (uint32_t)__builtin_amdgcn_s_memtime();
                     const uint32_t W = opaque((uint32_t)p.W);
                     int lr = (int)(L.item / W);
                     L.x = (int)(L.item - (uint32_t)lr * W);
@@ -142,7 +145,8 @@ __device__ __forceinline__ void end_path(Lane& L, const RenderParams& p) {
     const bool writer = split_writer<S>();
     if (p.frame_split) {  // frame_accumulate adds the frames in order afterwards
         if (writer) p.frame_buf[(size_t)L.frame * p.n_pix + L.item] = make_float4(c.x, c.y, c.z, 0.0f);
-        if (writer && p.cost_out) p.cost_out[L.item] = (uint32_t)__builtin_amdgcn_s_memtime() - p.cost_out[L.item];
+        if (writer && p.cost_out && L.frame == 0)
+            p.cost_out[L.item] = (uint32_t)__builtin_amdgcn_s_memtime() - p.cost_out[L.item];
         L.st = ST_NEED_ITEM;
         return;
     }

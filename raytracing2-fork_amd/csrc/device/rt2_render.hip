@@ -714,11 +714,19 @@ const Variant kVariants[] = {
     RT2_VARIANT(326, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = kt_res_spec(1); x.block = 768; x.waves = 3; return x; }()>, 768, "mfmar/768/kt1/res38/coop4/w3/cmp/dpp"),
     RT2_VARIANT(327, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = kt_res_spec(1); x.block = 768; x.waves = 3; x.prefetch = true; return x; }()>, 768, "mfmar/768/kt1/res38/coop4/w3/cmp/dpp/pf"),
     RT2_VARIANT(328, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = kt_res_spec(1); x.prefetch = true; return x; }()>, 1024, "mfmar/1024/kt1/res38/coop4/w4/cmp/dpp/pf"),
+    // ... schedule 4: the two 32-ray blocks interleaved (each wave's products beside its own reduction)
+    RT2_VARIANT(329, K_MFMA, render_mfma_k5r<kt_res_spec(4)>, 1024, "mfmar/1024/kt4/res38/coop4/w4/cmp/dpp"),
+    RT2_VARIANT(336, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = kt_res_spec(4); x.fair_prio = true; return x; }()>, 1024, "mfmar/1024/kt4/res38/coop4/w4/cmp/fair/dpp"),
+    RT2_VARIANT(337, K_MFMA, render_mfma_k5r<kt_res_spec(4, false, true)>, 1024, "mfmarl2/1024/kt4/res38l2/coop4/w4/cmp/dpp"),
+    RT2_VARIANT(338, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = kt_res_spec(4, false, true); x.fair_prio = true; return x; }()>, 1024, "mfmarl2/1024/kt4/res38l2/coop4/w4/cmp/fair/dpp"),
+    RT2_VARIANT(339, K_MFMA, render_mfma_k5r<kt_res_spec(4, true)>, 1024, "mfmar/1024/kt4/res38/coop4/w4/cmp/diag/dpp"),
     // ... on the LDS-tiled kernel (the form of 293): 19-group tiles at 3 waves per SIMD (schedules 1, 2), 16-group
     // tiles at 4 waves
     RT2_VARIANT(330, K_MFMA, render_mfma_k5t<kt_tiles_spec(19, 3, 1)>, 768, "mfmat5/768/kt1/tile19/coop0/w3/cmp/regs/perm"),
     RT2_VARIANT(331, K_MFMA, render_mfma_k5t<kt_tiles_spec(19, 3, 2)>, 768, "mfmat5/768/kt2/tile19/coop0/w3/cmp/regs/perm"),
+    RT2_VARIANT(332, K_MFMA, render_mfma_k5t<kt_tiles_spec(19, 3, 4)>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm"),
     RT2_VARIANT(333, K_MFMA, render_mfma_k5t<kt_tiles_spec(16, 4, 1)>, 1024, "mfmat5/1024/kt1/tile16/coop0/w4/cmp/regs/perm"),
+    RT2_VARIANT(335, K_MFMA, render_mfma_k5t<kt_tiles_spec(16, 4, 4)>, 1024, "mfmat5/1024/kt4/tile16/coop0/w4/cmp/regs/perm"),
     RT2_VARIANT(334, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 1); x.diag = true; return x; }()>, 768, "mfmat5/768/kt1/tile19/coop0/w3/cmp/regs/perm/diag"),
     RT2_VARIANT(299, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, true); x.fair_prio = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/fair/diag/dpp"),
     // earlier choices of rounds 3-4 (the 5-product form before and after the threshold moved into the accumulator,
@@ -1014,14 +1022,12 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
             p.n_runs = (uint32_t)runs;
         }
         // the cost map keeps each item's start clock in the pixel's own slot:
-        // with frame-major items several frames of one pixel run at once and
-        // would share it, so only whole-pixel launches measure
-        // (frame-split launches still use the order of an earlier map)
-        if (!p.frame_split) {
-            p.cost_out = s->d_cost;
-            s->cost_npix = p.n_pix;
-            std::memcpy(s->cost_key, key, sizeof(key));
-        }
+        // with frame-major items several frames of one pixel run at once, so
+        // only frame 0's item of each pixel measures (one
+        // writer per slot; a frame-split launch's map is its frame 0's cost)
+        p.cost_out = s->d_cost;
+        s->cost_npix = p.n_pix;
+        std::memcpy(s->cost_key, key, sizeof(key));
     }
     const size_t resident_bytes = (size_t)3 * sizeof(float4) * (size_t)std::max(s->n_tris, 1);
     const bool fits = resident_bytes <= kResidentMaxBytes;
@@ -1280,6 +1286,20 @@ extern "C" int rt2_scene_diag_ex(rt2_scene* s, unsigned long long* out, int n) {
     if (!s || !out || n < 0) return -1;
     std::memcpy(out, s->diag, sizeof(unsigned long long) * (size_t)std::min(n, kCounters));
     return std::min(n, kCounters);
+}
+
+// Not in rt2.h (test hook): the cost map of the last cost-ordered launch
+// (shader clocks per pixel of the slab) into `out` (n entries); returns the
+// pixels it describes (0 = no valid map), < 0 on error.
+extern "C" long long rt2_scene_cost_map(rt2_scene* s, uint32_t* out, unsigned long long n) {
+    if (!s) return -1;
+    if (!s->d_cost || s->cost_npix == 0) return 0;
+    if (out && n >= s->cost_npix) {
+        HIPCHECK(hipSetDevice(s->device));
+        HIPCHECK(hipDeviceSynchronize());
+        HIPCHECK(hipMemcpy(out, s->d_cost, s->cost_npix * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    }
+    return (long long)s->cost_npix;
 }
 
 // Not in rt2.h (diagnostics): whether the scene's triangles admit sweep_plk,

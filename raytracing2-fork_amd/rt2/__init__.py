@@ -622,6 +622,20 @@ class Scene:
         frags = frags.view(np.float16)
         return terms, (frags if layout >= 4 else np.ascontiguousarray(frags[:, :48])), rinfo, acc.astype(bool)
 
+    def cost_map(self) -> np.ndarray | None:
+        """The per-pixel cost map of the last cost-ordered launch (test hook
+        rt2_scene_cost_map; shader clocks), or None when there is none."""
+        fn = lib().rt2_scene_cost_map
+        fn.restype = C.c_longlong
+        fn.argtypes = [C.c_void_p, C.c_void_p, C.c_ulonglong]
+        n = fn(self._p, None, 0)
+        if n <= 0:
+            return None
+        out = np.zeros(n, dtype=np.uint32)
+        if fn(self._p, out.ctypes.data, n) != n:
+            raise RT2Error("rt2_scene_cost_map failed")
+        return out
+
     def stats(self, reset: bool = False) -> Stats:
         s = Stats()
         _check(lib().rt2_scene_stats(self._p, C.byref(s), int(reset)), "stats")

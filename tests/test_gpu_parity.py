@@ -462,13 +462,14 @@ def test_cost_ordered_renders_identical(rt2mod, oraclemod, config_scene, torch_c
     scene = rt2mod.Scene(sd, 0)
     scene.set_traversal(traversal)
     scene.set_cost_order(True)
-    if frames > 1:
-        # frame-major items write no cost map (several frames of a pixel run at
-        # once); they use the order of a whole-pixel launch's map
-        scene.render_host(u, 0, 1)
+    # frame-major launches too write the map (frame 0's item of each pixel
+    # measures: ADVICE r5), so a sequence of them is cost-ordered from the
+    # second render on without a whole-pixel launch first
     imgs = [scene.render_host(u, 0, frames, rgb8=True) for _ in range(3)]
+    cm = scene.cost_map()
+    assert cm is not None and len(cm) == W * H and (cm > 0).mean() > 0.99
     st = scene.stats(reset=True)
-    assert st.samples == 3 * W * H * 4 * frames + (W * H * 4 if frames > 1 else 0)
+    assert st.samples == 3 * W * H * 4 * frames
     for img, img8 in imgs[1:]:
         assert np.array_equal(img, imgs[0][0]) and np.array_equal(img8, imgs[0][1])
     ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(H), 0, frames, traversal)
