@@ -146,6 +146,11 @@ __device__ __forceinline__ bool sweep_kt_res(const RenderParams& p, const h8* re
             tb += kKtOps * 64;
             const unsigned long long M = kt_group<S>(a0, y1, b0, b1, b2, b3, upper);
             if constexpr (S.diag) dg.groups += 1;
+            if constexpr (S.sol == 2) {
+                // speed-of-light probe (WRONG images): no exact phase
+                if (M == 0x123456789ull) best = -best;
+                continue;
+            }
             if (M && exact_group<S>(M, G, n_tris, tri, o, d, best, bi, bestK, dg)) kt_y(d, o, bestK, sc, tw16, y1);
         }
     }
@@ -195,6 +200,8 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
     lane_init(L);
     MfmaDiag dg;
     const int wave = (int)(threadIdx.x >> 6);
+    // MfmaSpec::lean: the wave counts its lanes' segments (no per-lane counter)
+    [[maybe_unused]] unsigned long long segs_w = 0;
     // diag wave timeline (p.wave_log, render_mfma's 10-word layout: start,
     // first lane out of items, end, segment rounds with two 32-ray blocks /
     // one / - / cooperative drain, HW_ID | XCC_ID << 32, shader clocks)
@@ -205,8 +212,9 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
     }
     for (;;) {
         const RenderParams& p = kargs<RenderParams>();
-        advance(L, p);
+        advance<1, !S.lean>(L, p);
         unsigned long long act = __ballot(L.st == ST_TRACE);
+        if constexpr (S.lean) segs_w += (unsigned long long)__popcll(act);
         if constexpr (S.diag) {
             if (!wl_dry && __any(L.st == ST_DONE)) wl_dry = __builtin_amdgcn_s_memrealtime();
             if (act) {
@@ -225,7 +233,7 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
             coop_each(act, L.o, L.d, p, mybest, mybi);
             if (L.st == ST_TRACE) {
                 L.bounce += 1;
-                L.segs += 1;
+                if constexpr (!S.lean) L.segs += 1;
                 shade(L, p, mybest, mybi);
             }
             continue;
@@ -260,7 +268,7 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
                     const uint32_t l = lane_id(), nl = (uint32_t)__popcll(act);
                     const bool live = (act >> l) & 1ull;
                     const int to = 4 * (int)(live ? lanes_below(act) : nl + lanes_below(~act));
-                    lane_permute(L, to);
+                    lane_permute<!S.lean, !S.lean>(L, to);
                     act = __ballot(L.st == ST_TRACE);
                 }
                 upper = false;
@@ -290,12 +298,16 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
         if (!swept) coop_each(act, ro, rd, p, best, bi);
         if (mine) {
             L.bounce += 1;
-            L.segs += 1;
+            if constexpr (!S.lean) L.segs += 1;
             shade(L, p, best, bi);
         }
     }
     const RenderParams& p = kargs<RenderParams>();
-    flush_counters(L, p);
+    if constexpr (S.lean) {
+        if (lane_id() == 0) atomicAdd(p.seg_counter, segs_w);
+    } else {
+        flush_counters(L, p);
+    }
     if constexpr (S.diag)
         if (p.wave_log) {
             const uint32_t gw = blockIdx.x * NW + (uint32_t)wave;

@@ -84,6 +84,8 @@ struct MfmaSpec {
                              // left, quartiles of the rays per pixel (fair share among a SIMD's waves)
     int res_groups = 0;     // render_mfma_k5r (rt2_k5_resident.h): every group's records resident in the
                             // workgroup's LDS for the whole launch (scenes of <= res_groups 32-triangle groups)
+    bool lean = false;      // render_mfma_k5r: x, y recomputed from the item, segments counted per wave (fewer
+                            // VGPRs live across the sweep)
     int kthr = 0;           // the threshold in the K-slots (round 6, DESIGN.md "The threshold in the K-slots"):
                             // U, -V, X drop the m.y and m.z cross slots and carry -tau x Tw' and -B x W' in slots
                             // 14, 15; Y carries -tau x Tw' in slot 29: 8 products per group with a zero
@@ -555,11 +557,16 @@ __device__ __forceinline__ void lane_stash(const Lane& L, uint32_t (*st)[64], in
 __device__ __forceinline__ int perm_i(int to, int v) { return __builtin_amdgcn_ds_permute(to, v); }
 __device__ __forceinline__ float perm_f(int to, float v) { return __int_as_float(__builtin_amdgcn_ds_permute(to, __float_as_int(v))); }
 __device__ __forceinline__ f3 perm_f3(int to, const f3& v) { return mk(perm_f(to, v.x), perm_f(to, v.y), perm_f(to, v.z)); }
+// XY = false: the caller does not keep x, y (advance<S, false>); SEGS = false:
+// nor the per-lane segment count (MfmaSpec::lean)
+template <bool XY = true, bool SEGS = true>
 __device__ __forceinline__ void lane_permute(Lane& L, int to) {
     L.st = perm_i(to, L.st);
     L.item = (uint32_t)perm_i(to, (int)L.item);
-    L.x = perm_i(to, L.x);
-    L.y = perm_i(to, L.y);
+    if constexpr (XY) {
+        L.x = perm_i(to, L.x);
+        L.y = perm_i(to, L.y);
+    }
     L.frame = (uint32_t)perm_i(to, (int)L.frame);
     L.seed = (uint32_t)perm_i(to, (int)L.seed);
     L.ray = perm_i(to, L.ray);
@@ -570,7 +577,7 @@ __device__ __forceinline__ void lane_permute(Lane& L, int to) {
     L.rayColor = perm_f3(to, L.rayColor);
     L.incoming = perm_f3(to, L.incoming);
     L.colorCum = perm_f3(to, L.colorCum);
-    L.segs = (uint32_t)perm_i(to, (int)L.segs);
+    if constexpr (SEGS) L.segs = (uint32_t)perm_i(to, (int)L.segs);
 }
 // lane_lds = 2: 15 words (st:3 inside:1 bounce:12 ray:16 | item | x:16 y:16 |
 // frame | seed | colours | segs); the launcher uses it
@@ -898,10 +905,10 @@ __device__ __forceinline__ void kt_y(const f3& d, const f3& o, float bkv, const 
 template <MfmaSpec S>
 __device__ __forceinline__ unsigned long long kt_group(const h8* a0, const h8* y1, const h8& bu, const h8& bv,
                                                        const h8& bx, const h8& bt, bool upper) {
-    static_assert(S.kthr >= 1 && S.kthr <= 4, "kthr schedule");
+    static_assert(S.kthr >= 1 && S.kthr <= 5, "kthr schedule");
     const f16v zero = {};
     int acc = 0;
-    if constexpr (S.kthr == 4) {
+    if constexpr (S.kthr == 4 || S.kthr == 5) {
         // kthr 4: the two blocks interleaved so that each wave's own products
         // run beside its own reduction VALU, at cthr's register peak (48
         // product VGPRs): [U0 V0 X0] [AND0] [Y0 U1] [fold0] [V1 X1] [AND1]
@@ -911,9 +918,20 @@ __device__ __forceinline__ unsigned long long kt_group(const h8* a0, const h8* y
             for (int i = 0; i < 16; i++)
                 t3[i] = __builtin_amdgcn_bitop3_b32(__float_as_int(U[i]), __float_as_int(V[i]), __float_as_int(X[i]), 0x80);
         };
-        auto fold = [](const int* t3, const f16v& Y, int a) {
+        // kthr 5: the fold as two interleaved chains (even / odd pairs), ORed
+        // at the group's end: half the dependent-VALU latency, one VALU more
+        int acc2 = 0;
+        auto fold = [&](const int* t3, const f16v& Y, int a) {
+            if constexpr (S.kthr == 5) {
 #pragma unroll
-            for (int i = 0; i < 16; i++) a = __builtin_amdgcn_bitop3_b32(t3[i], __float_as_int(Y[i]), a, 0xEA);
+                for (int i = 0; i < 16; i += 2) {
+                    a = __builtin_amdgcn_bitop3_b32(t3[i], __float_as_int(Y[i]), a, 0xEA);
+                    acc2 = __builtin_amdgcn_bitop3_b32(t3[i + 1], __float_as_int(Y[i + 1]), acc2, 0xEA);
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 16; i++) a = __builtin_amdgcn_bitop3_b32(t3[i], __float_as_int(Y[i]), a, 0xEA);
+            }
             return a;
         };
         if (upper) {
@@ -947,6 +965,7 @@ __device__ __forceinline__ unsigned long long kt_group(const h8* a0, const h8* y
             const f16v Y0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(y1[0], bt, zero, 0, 0, 0);
             acc = fold(t0, Y0, acc);
         }
+        if constexpr (S.kthr == 5) acc |= acc2;
         return __ballot(acc < 0);
     }
 #pragma unroll

@@ -31,9 +31,21 @@ __device__ __forceinline__ bool split_writer() {
 template <int S = 1>
 __device__ __forceinline__ void end_path(Lane& L, const RenderParams& p);
 
+// The pixel of item `item` (row-major in the slab; rows interleaved over
+// ranks in tiles)
+__device__ __forceinline__ void item_xy(uint32_t item, const RenderParams& p, int& x, int& y) {
+    const uint32_t W = opaque((uint32_t)p.W);
+    const int lr = (int)(item / W);
+    x = (int)(item - (uint32_t)lr * W);
+    y = shard_row(lr, p.tile_rows, p.rank, p.nranks);
+}
+
 // Phase A: bring every lane to ST_TRACE or ST_DONE (wave-collective; with
 // S > 1 workgroup-collective, every wave of the group on the same path).
-template <int S = 1>
+// XY = false: L.x, L.y are not kept across calls (recomputed from L.item
+// where a new frame or ray needs them: two VGPRs less live across the sweep
+// of the register-bound resident kernel)
+template <int S = 1, bool XY = true>
 __device__ __forceinline__ void advance(Lane& L, const RenderParams& p) {
     for (;;) {
         const bool need = L.st == ST_NEED_ITEM;
@@ -87,10 +99,7 @@ __device__ __forceinline__ void advance(Lane& L, const RenderParams& p) {
                     // slot: the pixel's other frames run at the same time)
                     if (p.cost_out && split_writer<S>() && f == 0u)
                         p.cost_out[L.item] = (uint32_t)__builtin_amdgcn_s_memtime();
-                    const uint32_t W = opaque((uint32_t)p.W);
-                    int lr = (int)(L.item / W);
-                    L.x = (int)(L.item - (uint32_t)lr * W);
-                    L.y = shard_row(lr, p.tile_rows, p.rank, p.nranks);
+                    if constexpr (XY) item_xy(L.item, p, L.x, L.y);
                     L.frame = f;
                     L.st = ST_NEW_FRAME;
                 } else {
@@ -98,6 +107,8 @@ __device__ __forceinline__ void advance(Lane& L, const RenderParams& p) {
                 }
             }
         }
+        if constexpr (!XY)
+            if (L.st == ST_NEW_FRAME || L.st == ST_NEW_RAY) item_xy(L.item, p, L.x, L.y);
         if (L.st == ST_NEW_FRAME) {
             // compute.glsl:662-670
             const uint32_t f = p.frame_begin + L.frame;

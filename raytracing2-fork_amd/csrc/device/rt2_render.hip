@@ -599,7 +599,7 @@ constexpr MfmaSpec kMfmaK5NoTnW4 = [] {
 // the small-scene kernel (233) with the cooperative drain at <= 4 live rays
 // instead of 8 (config B 189.5 vs 194.4 ms, 1/8 slab 29.0 vs 29.4 ms;
 // profiles/r03_coop_ab_configB.json, r03_coop_shard_probe_configB.jsonl)
-constexpr MfmaSpec kMfmaK5NoTnW4C4 = [] {
+[[maybe_unused]] constexpr MfmaSpec kMfmaK5NoTnW4C4 = [] {
     MfmaSpec x = kMfmaK5NoTnW4;
     x.tail_lanes = 4;
     return x;
@@ -655,6 +655,13 @@ constexpr MfmaSpec kt_tiles_spec(int K, int waves, int sched) {
     x.kthr = sched;
     return x;
 }
+// the round-6 defaults: kthr 4, the lean lane state; l2 = the L2 continuation (39..256 groups), fair = rank slabs
+constexpr MfmaSpec kt_res_lean(bool l2, bool fair) {
+    MfmaSpec x = kt_res_spec(4, false, l2);
+    x.lean = true;
+    x.fair_prio = fair;
+    return x;
+}
 constexpr int kResL2Groups = 256;  // render_mfma_k5r with res_l2: 38 groups resident, the rest from L2
 constexpr Bvh3Spec kBvhDefault{.block = 256, .thresh = 16, .slab = Slab::Markstein, .waves = 5, .diag = false};
 
@@ -679,7 +686,20 @@ const Variant kVariants[] = {
     // default brute-force kernel (DESIGN.md "The 5-product form"): the k16 sweep with U, -V, X from the first K-half,
     // the left-out m.z slots bounded in the threshold; 3 waves per SIMD, and 4 for launches with < 1.5 items per lane
     RT2_VARIANT(227, K_MFMA, render_mfma<kMfmaK5>, 256, "mfma/256/k5/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp"),
-    // scenes of <= 8,192 triangles (records L2-resident): the same without the -tn term (4 products per block) and
+    // scenes of <= 256 groups (8,192 triangles; config B: 38, W: 57, K: 89): the resident kernel (rt2_k5_resident.h:
+    // records in LDS for the whole launch, 38 groups, the rest read from L2) with the threshold in the K-slots
+    // (MfmaSpec::kthr 4: 8 independent products per group, the two 32-ray blocks interleaved; DESIGN.md "The
+    // threshold in the K-slots"), the lean lane state; fair-share issue priority for rank slabs
+    RT2_VARIANT(342, K_MFMA, render_mfma_k5r<kt_res_lean(false, false)>, 1024, "mfmar/1024/kt4/res38/coop4/w4/cmp/dpp/lean"),
+    RT2_VARIANT(344, K_MFMA, render_mfma_k5r<kt_res_lean(false, true)>, 1024, "mfmar/1024/kt4/res38/coop4/w4/cmp/fair/dpp/lean"),
+    RT2_VARIANT(345, K_MFMA, render_mfma_k5r<kt_res_lean(true, false)>, 1024, "mfmarl2/1024/kt4/res38l2/coop4/w4/cmp/dpp/lean"),
+    RT2_VARIANT(346, K_MFMA, render_mfma_k5r<kt_res_lean(true, true)>, 1024, "mfmarl2/1024/kt4/res38l2/coop4/w4/cmp/fair/dpp/lean"),
+    // the default above 8,192 triangles (round 5): 217 with the fragments built in registers (no LDS rows), so the
+    // tiles hold 19 groups
+    RT2_VARIANT(293, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(19, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; x.perm_frag = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile19/coop0/w3/cmp/regs/cthr/perm"),
+#ifdef RT2_EXPERIMENTS
+    // the defaults of rounds 4-5 (round 6 replaced them by the kthr resident kernels 342-346)
+    // (round 4) scenes of <= 8,192 triangles (records L2-resident): the same without the -tn term (4 products per block) and
     // with the threshold in the products' accumulator (MfmaSpec::cthr, DESIGN.md "The threshold in the
     // accumulator"), 4 waves (packed path state, Y fragments read per block: 263), or 3 when the packed fields do not
     // hold the image / rays / bounces (262)
@@ -694,10 +714,6 @@ const Variant kVariants[] = {
     // ... with fair-share issue priority (rank slabs: < kResSlabItems items per lane; DESIGN.md "Fair-share issue
     // priority")
     RT2_VARIANT(298, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4); x.fair_prio = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/fair/dpp"),
-    // the default above 8,192 triangles (round 5): 217 with the fragments built in registers (no LDS rows), so the
-    // tiles hold 19 groups
-    RT2_VARIANT(293, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(19, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; x.perm_frag = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile19/coop0/w3/cmp/regs/cthr/perm"),
-#ifdef RT2_EXPERIMENTS
     // records resident in LDS at 3 waves per SIMD; the resident kernel's diagnostic counters
     RT2_VARIANT(280, K_MFMA, render_mfma_k5r<k5_res_spec(3)>, 768, "mfmar/768/k5/notn/res38/coop4/w3/cmp/cthr/dpp"),
     RT2_VARIANT(287, K_MFMA, render_mfma_k5r<k5_res_spec(4, true)>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/diag/dpp"),
@@ -720,6 +736,13 @@ const Variant kVariants[] = {
     RT2_VARIANT(337, K_MFMA, render_mfma_k5r<kt_res_spec(4, false, true)>, 1024, "mfmarl2/1024/kt4/res38l2/coop4/w4/cmp/dpp"),
     RT2_VARIANT(338, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = kt_res_spec(4, false, true); x.fair_prio = true; return x; }()>, 1024, "mfmarl2/1024/kt4/res38l2/coop4/w4/cmp/fair/dpp"),
     RT2_VARIANT(339, K_MFMA, render_mfma_k5r<kt_res_spec(4, true)>, 1024, "mfmar/1024/kt4/res38/coop4/w4/cmp/diag/dpp"),
+    // ... the fold as two chains (kthr 5); speed-of-light probe without the exact phase (WRONG images: A/B with
+    // --no-check)
+    RT2_VARIANT(340, K_MFMA, render_mfma_k5r<kt_res_spec(5)>, 1024, "mfmar/1024/kt5/res38/coop4/w4/cmp/dpp"),
+    RT2_VARIANT(341, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = kt_res_spec(4); x.sol = 2; return x; }()>, 1024, "mfmar/1024/kt4/res38/coop4/w4/cmp/dpp/sol2"),
+    // ... with the lean lane state (x, y from the item, segments counted per wave)
+    RT2_VARIANT(342, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = kt_res_spec(4); x.lean = true; return x; }()>, 1024, "mfmar/1024/kt4/res38/coop4/w4/cmp/dpp/lean"),
+    RT2_VARIANT(343, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = kt_res_spec(5); x.lean = true; return x; }()>, 1024, "mfmar/1024/kt5/res38/coop4/w4/cmp/dpp/lean"),
     // ... on the LDS-tiled kernel (the form of 293): 19-group tiles at 3 waves per SIMD (schedules 1, 2), 16-group
     // tiles at 4 waves
     RT2_VARIANT(330, K_MFMA, render_mfma_k5t<kt_tiles_spec(19, 3, 1)>, 768, "mfmat5/768/kt1/tile19/coop0/w3/cmp/regs/perm"),
@@ -780,23 +803,26 @@ constexpr int kDefaultBrute = 0;
 constexpr int kDefaultBvh = 109;
 constexpr int kLargeScene = 86;  // tiled/512/max3f4: LDS tiles above kSmemMaxTris triangles
 constexpr int kSlab = 92;        // assist12/max3f8/w6: fewer than 4 items per lane (multi-GPU slabs)
-constexpr int kMfmaSlabMaxTris = 8192;
-constexpr int kMfmaSmall = 263;    // <= kMfmaSlabMaxTris triangles: k5 without -tn, 4 waves (packed path state),
-                                   // cooperative drain at <= 4 live rays (config B 187.9 vs 192.9 ms for 233's 8), the
-                                   // threshold in the accumulator (DESIGN.md "The threshold in the accumulator")
-constexpr int kMfmaRes = 282;      // <= kResGroups groups (config B): every record resident in LDS, 4 waves per SIMD
-                                   // (rt2_k5_resident.h): config B 164.6 vs 189.7 ms for 263, identical image
-constexpr int kMfmaResSlab = 298;  // ... launches with < kResSlabItems items per resident lane (rank slabs): the
-                                   // same kernel with fair-share issue priority (MfmaSpec::fair_prio): config B 1/8
-                                   // slab 23.5 vs 25.5 ms, 1/2 85.8 vs 88.7 ms; whole images unchanged or ~1 % slower
+constexpr int kMfmaSlabMaxTris = 8192;  // = kResL2Groups x 32: the resident kernel with its L2 continuation
+constexpr int kMfmaRes = 342;      // <= kResGroups groups (config B): every record resident in LDS, 4 waves per SIMD,
+                                   // the threshold in the K-slots (kthr 4), the lean lane state (rt2_k5_resident.h;
+                                   // DESIGN.md "The threshold in the K-slots"): config B 146.9-149.4 vs 154.2-165.3 ms
+                                   // for round 5's 282 in A/Bs on two boxes, identical image
+constexpr int kMfmaResSlab = 344;  // ... launches with < kResSlabItems items per resident lane (rank slabs): the
+                                   // same kernel with fair-share issue priority (MfmaSpec::fair_prio; round 5: 298)
 constexpr unsigned long long kResSlabItems = 6;
-constexpr int kMfmaSmallW3 = 262;  // ... 3 waves, when the packed fields cannot hold the launch
+constexpr int kMfmaResL2 = 345;    // 39..256 groups (configs W, K): 38 groups resident, the rest read from L2
+                                   // (MfmaSpec::res_l2): config W 28.7 vs 46.5 ms, K 306.8 vs 362.1 ms for round 4-5's
+                                   // L2-resident 263 (A/B, identical images)
+constexpr int kMfmaResL2Slab = 346;  // ... its rank slabs (fair-share priority)
 constexpr int kMfmaTiles = 293;    // larger scenes (round 5): 217's LDS tiles with the fragments built in registers
                                    // (v_permlane32_swap, no LDS rows), so the tiles grow to 19 groups: config C
                                    // 23.63 vs 23.87 s, config E 6.14 vs 6.23 s (same images); round 4's 217:
-                                   // the 5-product form without -tn with workgroup-shared LDS record tiles of 10 groups, the path state in registers (rt2_k5_tiles.h; DESIGN.md "LDS
-                                   // record tiles": config C 25.94 vs 26.66 s for 252's 4-group tiles and 32.5 s for
-                                   // round 3's 227), the threshold in the accumulator (C sample 1.07 vs 1.24 s for 213)
+                                   // the 5-product form without -tn with workgroup-shared LDS record tiles of 10
+                                   // groups, the path state in registers (rt2_k5_tiles.h; DESIGN.md "LDS record
+                                   // tiles"), the threshold in the accumulator.  The kthr form does not pay here
+                                   // (C sample 1,049 vs 1,049 ms, E 1,228 vs 1,206 ms: DESIGN.md "The threshold in
+                                   // the K-slots")
 constexpr int kMfma = 227;  // mfma/.../k5/...: the matrix-core filter on v_mfma_f32_32x32x16_f16, 5 products per
                             // 32-ray block (DESIGN.md "The 5-product form"), registers only; larger scenes whose
                             // packed path state cannot hold the launch
@@ -1056,32 +1082,24 @@ extern "C" int rt2_render(rt2_scene* s, const rt2_uniforms* u, uint32_t frame_be
             // slabs' tails) and every scene size: config E's 1M triangles too
             // (3.9 vs 6.9 s for kLargeScene on a 480x270 sample)
             vi = kMfma;
-            // scenes whose records stay L2-resident (<= 8,192 triangles: config
-            // B): without the -tn term, whose exact tests cost less there than
-            // its product (config B 195 vs 214 ms), and at 4 waves per SIMD, which
-            // packs the path state into 16-bit fields (x, y, rays per pixel)
-            // and 12 bits of bounce count: whole images and rank slabs alike
-            // (config B 195 vs 200 ms at 3 waves; 1/8 slab 29.4 vs 34.6 ms).
-            // At config C's 100k triangles the fourth wave costs more than its
-            // lanes gain (a 480x270x2 sample, 1.3 items per lane: 3.13 vs
-            // 2.13 s for the k16 sweep)
-            // Larger scenes stream their records from the MALL unless the
-            // workgroup shares them: the LDS-tiled kernel (one 12-wave
-            // workgroup per CU), without the -tn term (config C 26.94 vs
-            // 29.19 s with it; config E sample 1.56 vs 1.60 s); its path state
-            // stays in registers, so it has no packed-field limits
-            if (res_fits && find_variant(kMfmaRes)) {
-                vi = kMfmaRes;
+            // Scenes of up to 256 groups: the resident kernel (its path state
+            // in registers: no packed-field limits).  Larger scenes stream
+            // their records from the MALL unless the workgroup shares them:
+            // the LDS-tiled kernel (one 12-wave workgroup per CU), without the
+            // -tn term (config C 26.94 vs 29.19 s with it; config E sample
+            // 1.56 vs 1.60 s); its path state stays in registers too
+            if (s->n_tris <= kMfmaSlabMaxTris) {
+                // the resident kernel: every group resident in LDS (<= 38) or
+                // the first 38 resident and the rest read from L2 (<= 256);
                 // a SIMD's waves start together with a few items per lane:
                 // fair share, so that they also end together (DESIGN.md
                 // "Fair-share issue priority")
                 const unsigned long long lanes = (unsigned long long)s->num_cus * (unsigned long long)find_variant(kMfmaRes)->block;
-                if (p.n_items < kResSlabItems * lanes && find_variant(kMfmaResSlab)) vi = kMfmaResSlab;
-            }
-            else if (s->n_tris <= kMfmaSlabMaxTris)
-                vi = packed && find_variant(kMfmaSmall) ? kMfmaSmall : kMfmaSmallW3;
-            else if (find_variant(kMfmaTiles))
+                const bool slab = p.n_items < kResSlabItems * lanes;
+                vi = res_fits ? (slab ? kMfmaResSlab : kMfmaRes) : (slab ? kMfmaResL2Slab : kMfmaResL2);
+            } else if (find_variant(kMfmaTiles)) {
                 vi = kMfmaTiles;
+            }
         } else if (vi == kDefaultBrute) {
             // scenes outside the matrix filter's range (mfma_ok = 0):
             // items per resident lane decide the tail: a lane ends on a whole

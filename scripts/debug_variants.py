@@ -15,7 +15,7 @@ import rt2  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="A")
-ap.add_argument("--variants", default="282,320")
+ap.add_argument("--variants", default="282,342")
 ap.add_argument("--width", type=int, default=0)
 ap.add_argument("--height", type=int, default=0)
 ap.add_argument("--rays", type=int, default=0)

@@ -14,14 +14,14 @@ pytestmark = pytest.mark.gpu
 
 MFMA = 227
 # every matrix-filter variant of the loaded library runs each case: the
-# product build's automatic kernels (227, 262, 263, the LDS-resident 282 and
-# the LDS-tiled 217 / 293); the experiment build adds its A/B variants
+# product build's automatic kernels (227, the resident 342 / 344 and their L2
+# continuation 345 / 346, the LDS-tiled 293); the experiment build adds its A/B variants
 # (other drain thresholds, wave counts, record tiles, the kthr forms 320-325)
 
 
 def _mfma_variants():
     """Every matrix-filter variant the loaded library carries (ids 130-399:
-    the product defaults 262 / 263 / 282 / 293 included)."""
+    the product defaults 342-346 / 293 included)."""
     import rt2
     out = []
     for v in range(130, 400):

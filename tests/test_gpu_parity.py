@@ -130,10 +130,10 @@ def _last_variant(rt2mod, scene):
 
 
 AUTO_TILES = "mfmat5/768/k5/notn/tile19/coop0/w3/cmp/regs/cthr/perm"  # variant 293: > 8,192 triangles, LDS record tiles
-AUTO_RES = "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/dpp"  # 282: <= 38 groups (1,216 triangles), records resident in LDS
-AUTO_RES_SLAB = "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/fair/dpp"  # 298: the same, < 6 items per lane (rank slabs)
-AUTO_SMALL = "mfma/256/k5/notn/coop4/w4/imax/minred/ymma/t12/llds2/ser4/cmp/cthr/yl1"  # 263: <= 8,192 triangles
-AUTO_SMALL_W3 = "mfma/256/k5/notn/coop8/w3/imax/minred/ymma/t12/llds/ser4/cmp/cthr"  # 262: packed fields too small
+AUTO_RES = "mfmar/1024/kt4/res38/coop4/w4/cmp/dpp/lean"  # 342: <= 38 groups (1,216 triangles), records resident in LDS
+AUTO_RES_SLAB = "mfmar/1024/kt4/res38/coop4/w4/cmp/fair/dpp/lean"  # 344: the same, < 6 items per lane (rank slabs)
+AUTO_RES_L2 = "mfmarl2/1024/kt4/res38l2/coop4/w4/cmp/dpp/lean"  # 345: 39..256 groups, the rest from L2
+AUTO_RES_L2_SLAB = "mfmarl2/1024/kt4/res38l2/coop4/w4/cmp/fair/dpp/lean"  # 346: its rank slabs
 
 
 def test_auto_variant_large_scene(rt2mod, oraclemod, config_scene, torch_cuda):
@@ -158,7 +158,7 @@ def _scene_between_res_and_tiles(rt2mod, config_scene):
     """Config B's scene plus 800 small triangles behind the camera (at z 11-14;
     it sits at z = 10 looking down -z): 2,008
     triangles, above the LDS-resident kernel's 38 groups and below the tiled
-    kernel's 8,192 (the L2-resident 4-wave kernel's range)."""
+    kernel's 8,192 (the range of the resident kernel's L2 continuation)."""
     _, spec = config_scene("B")
     sd, _ = rt2mod.build_config_scene("B")  # a fresh copy (config_scene's is shared)
     rng = np.random.default_rng(3)
@@ -168,12 +168,12 @@ def _scene_between_res_and_tiles(rt2mod, config_scene):
     return sd, spec
 
 
-@pytest.mark.parametrize("extra,want", [(8, "res"), (9, "small")], ids=["1216-tris", "1217-tris"])
+@pytest.mark.parametrize("extra,want", [(8, "res"), (9, "l2")], ids=["1216-tris", "1217-tris"])
 def test_auto_variant_resident_boundary(rt2mod, oraclemod, torch_cuda, extra, want):
-    """The LDS-resident kernel holds scenes of at most 38 groups (1,216
-    triangles): config B's 1,208 triangles plus 8 take it, plus 9 (a 39th
-    group of one triangle) take the L2-resident 4-wave kernel — bit-exact
-    either way, the last group's padding included."""
+    """The LDS holds the records of 38 groups (1,216 triangles): config B's
+    1,208 triangles plus 8 take the all-resident kernel, plus 9 (a 39th group
+    of one triangle) its L2 continuation — bit-exact either way, the last
+    group's padding included (a small image: the rank-slab builds)."""
     sd, spec = rt2mod.build_config_scene("B")
     for i in range(extra):  # small triangles behind the camera (z = 10, looking down -z)
         x = -3.0 + 0.7 * i
@@ -182,29 +182,34 @@ def test_auto_variant_resident_boundary(rt2mod, oraclemod, torch_cuda, extra, wa
     u = rt2mod.offline_uniforms(64, 36, spec.bounces, 4, sd.num_triangles)
     scene = rt2mod.Scene(sd, 0)
     img = scene.render_host(u, 0, 1)
-    assert _last_variant(rt2mod, scene) == (AUTO_RES_SLAB if want == "res" else AUTO_SMALL)
+    assert _last_variant(rt2mod, scene) == (AUTO_RES_SLAB if want == "res" else AUTO_RES_L2_SLAB)
     ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(36), 0, 1)
     assert_exact(img, ref, f"{sd.num_triangles} triangles")
 
 
-def test_auto_variant_packed_state_limits(rt2mod, oraclemod, config_scene, torch_cuda):
-    """Scenes between 38 and 256 groups run the 4-wave L2-resident build, whose
-    path state packs the bounce count into 12 bits; a bounce limit above 4095
-    takes the 3-wave build of the same form — same image either way."""
+def test_auto_variant_l2_continuation(rt2mod, oraclemod, config_scene, torch_cuda):
+    """Scenes between 38 and 256 groups run the resident kernel's L2
+    continuation, whose path state stays in registers: a bounce limit of 5000
+    (beyond the 12-bit packed fields of round 4-5's 263) takes the same kernel
+    — same image as the oracle either way; a whole image takes the build
+    without fair-share priority."""
     sd, spec = _scene_between_res_and_tiles(rt2mod, config_scene)
     assert 38 * 32 < sd.num_triangles <= 8192
     u = rt2mod.offline_uniforms(40, 24, spec.bounces, 3, sd.num_triangles)
     scene = rt2mod.Scene(sd, 0)
     img = scene.render_host(u, 0, 1)
-    assert _last_variant(rt2mod, scene) == AUTO_SMALL
+    assert _last_variant(rt2mod, scene) == AUTO_RES_L2_SLAB
     u.maxBounceCount = 5000
     img2 = scene.render_host(u, 0, 1)
-    assert _last_variant(rt2mod, scene) == AUTO_SMALL_W3
+    assert _last_variant(rt2mod, scene) == AUTO_RES_L2_SLAB
     ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(24), 0, 1)
     assert_exact(img2, ref, "5000 bounces")
     u.maxBounceCount = spec.bounces
     ref, _, _ = oracle_mean(oraclemod, sd, u, np.arange(24), 0, 1)
-    assert_exact(img, ref, "packed state")
+    assert_exact(img, ref, "L2 continuation")
+    uw = rt2mod.offline_uniforms(spec.width, spec.height, spec.bounces, 1, sd.num_triangles)
+    scene.render_host(uw, 0, 1)
+    assert _last_variant(rt2mod, scene) == AUTO_RES_L2
 
 
 def test_auto_variant_by_items_per_lane(rt2mod, config_scene, torch_cuda):
@@ -399,13 +404,13 @@ def test_frame_split_identical(rt2mod, oraclemod, config_scene, torch_cuda, trav
 
 
 # brute-force kernel variants that change the schedule, not the arithmetic:
-# the product variants (0 = automatic, 86, 92, 227/262/263 = the matrix filter, 217/293 = its LDS-tiled forms,
-# 282/298 = its LDS-resident forms, 136 = the scalar path forced) and, in an experiment build, the A/B
+# the product variants (0 = automatic, 86, 92, 227 = the matrix filter, 293 = its LDS-tiled form, 342/344 = its
+# LDS-resident forms and 345/346 their L2 continuation, 136 = the scalar path forced) and, in an experiment build, the A/B
 # variants (masked/plk filters, resident LDS, cooperative and team tail modes,
 # split waves, the round-1 slab kernels, occupancy hints)
-BRUTE_VARIANTS = [0, 86, 92, 217, 227, 262, 263, 282, 293, 298, 136] + (
-    [213, 231, 243, 252, 260, 261, 212, 246, 228, 233, 250, 280, 320, 321, 322, 323, 325, 67, 85, 106, 64, 66, 74, 76,
-     79, 80] if EXPERIMENTS else [])
+BRUTE_VARIANTS = [0, 86, 92, 227, 293, 342, 344, 345, 346, 136] + (
+    [217, 262, 263, 282, 298, 213, 231, 243, 252, 260, 261, 212, 246, 228, 233, 250, 280, 320, 321, 322, 323, 325, 326,
+     327, 328, 329, 336, 337, 338, 340, 343, 67, 85, 106, 64, 66, 74, 76, 79, 80] if EXPERIMENTS else [])
 
 
 @pytest.mark.parametrize("variant", BRUTE_VARIANTS)
