@@ -50,6 +50,33 @@ __device__ __forceinline__ bool exact_group(unsigned long long M, int G, int n_t
     if constexpr (S.diag) dg.hot += 1;
     uint32_t m32 = (uint32_t)(M | M >> 32);
     const float bk0 = bestK;
+    if constexpr (S.exact_pf) {
+        // MfmaSpec::exact_pf: the next triangle's record is requested (vector
+        // loads of one uniform address: in-order vmcnt, unlike the scalar
+        // cache's) before this one is tested, so its latency overlaps the test
+        const float4* tv = reinterpret_cast<const float4*>((const float*)tri);
+        int tt = __builtin_ctz(m32);
+        m32 &= m32 - 1;
+        int idx = 32 * G + tt;
+        if (idx >= n_tris) return false;
+        float4 c0 = tv[3 * idx], c1 = tv[3 * idx + 1], c2 = tv[3 * idx + 2];
+        for (;;) {
+            int nidx = n_tris;
+            float4 n0 = c0, n1 = c1, n2 = c2;
+            if (m32) {
+                nidx = 32 * G + __builtin_ctz(m32);
+                m32 &= m32 - 1;
+                if (nidx < n_tris) n0 = tv[3 * nidx], n1 = tv[3 * nidx + 1], n2 = tv[3 * nidx + 2];
+            }
+            if constexpr (S.diag) dg.exact += 1;
+            const MtQ qq = mt_quantities(o, d, c0, c1, c2);
+            if (mt_pass3(qq, bestK)) mt_exact(qq, idx, best, bi, bestK);
+            if (nidx >= n_tris) break;
+            idx = nidx;
+            c0 = n0, c1 = n1, c2 = n2;
+        }
+        return __ballot(bestK != bk0) != 0;
+    }
     while (m32) {
         const int tt = __builtin_ctz(m32);
         m32 &= m32 - 1;

@@ -84,6 +84,7 @@ struct MfmaSpec {
                              // left, quartiles of the rays per pixel (fair share among a SIMD's waves)
     int res_groups = 0;     // render_mfma_k5r (rt2_k5_resident.h): every group's records resident in the
                             // workgroup's LDS for the whole launch (scenes of <= res_groups 32-triangle groups)
+    bool exact_pf = false;  // render_mfma_k5r: the exact phase requests the next triangle before testing this one
     bool lean = false;      // render_mfma_k5r: x, y recomputed from the item, segments counted per wave (fewer
                             // VGPRs live across the sweep)
     int kthr = 0;           // the threshold in the K-slots (round 6, DESIGN.md "The threshold in the K-slots"):

@@ -743,6 +743,8 @@ const Variant kVariants[] = {
     // ... with the lean lane state (x, y from the item, segments counted per wave)
     RT2_VARIANT(342, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = kt_res_spec(4); x.lean = true; return x; }()>, 1024, "mfmar/1024/kt4/res38/coop4/w4/cmp/dpp/lean"),
     RT2_VARIANT(343, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = kt_res_spec(5); x.lean = true; return x; }()>, 1024, "mfmar/1024/kt5/res38/coop4/w4/cmp/dpp/lean"),
+    // ... the exact phase with the next triangle requested ahead (vector loads)
+    RT2_VARIANT(347, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = kt_res_lean(false, false); x.exact_pf = true; return x; }()>, 1024, "mfmar/1024/kt4/res38/coop4/w4/cmp/dpp/lean/xpf"),
     // ... on the LDS-tiled kernel (the form of 293): 19-group tiles at 3 waves per SIMD (schedules 1, 2), 16-group
     // tiles at 4 waves
     RT2_VARIANT(330, K_MFMA, render_mfma_k5t<kt_tiles_spec(19, 3, 1)>, 768, "mfmat5/768/kt1/tile19/coop0/w3/cmp/regs/perm"),
