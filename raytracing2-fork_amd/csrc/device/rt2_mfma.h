@@ -85,6 +85,7 @@ struct MfmaSpec {
     int res_groups = 0;     // render_mfma_k5r (rt2_k5_resident.h): every group's records resident in the
                             // workgroup's LDS for the whole launch (scenes of <= res_groups 32-triangle groups)
     bool exact_pf = false;  // render_mfma_k5r: the exact phase requests the next triangle before testing this one
+    bool kt_lane_w = false; // kthr: the B_q slot's ray factor W per ray (its own mw_y + mw_z), not the wave's maximum
     bool lean = false;      // render_mfma_k5r: x, y recomputed from the item, segments counted per wave (fewer
                             // VGPRs live across the sweep)
     int kthr = 0;           // the threshold in the K-slots (round 6, DESIGN.md "The threshold in the K-slots"):
@@ -886,7 +887,10 @@ template <MfmaSpec S>
 __device__ __forceinline__ void kt_frags(const f3& d, const f3& m, const MfmaScale& sc, h8 a0[2], _Float16& tw16) {
     constexpr float pad = 1.00390625f;  // 1 + 2^-8 (the f32 sum mw_y + mw_z and the scale product round)
     _Float16 s[16];
-    const float W = wave_max_s<S>(kt_main_slots(s, d, m, sc.sigma));
+    // MfmaSpec::kt_lane_w: each ray's fragment carries its own mw_y + mw_z
+    // (the bound is per (ray, triangle) product: no wave maximum needed)
+    const float Wl = kt_main_slots(s, d, m, sc.sigma);
+    const float W = S.kt_lane_w ? Wl : wave_max_s<S>(Wl);
     tw16 = f16_up(sc.Tw * pad);
     s[14] = tw16;
     s[15] = f16_up(W * pad);

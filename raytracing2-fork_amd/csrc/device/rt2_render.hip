@@ -745,6 +745,10 @@ const Variant kVariants[] = {
     RT2_VARIANT(343, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = kt_res_spec(5); x.lean = true; return x; }()>, 1024, "mfmar/1024/kt5/res38/coop4/w4/cmp/dpp/lean"),
     // ... the exact phase with the next triangle requested ahead (vector loads)
     RT2_VARIANT(347, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = kt_res_lean(false, false); x.exact_pf = true; return x; }()>, 1024, "mfmar/1024/kt4/res38/coop4/w4/cmp/dpp/lean/xpf"),
+    // ... W per ray (kt_lane_w: a tighter threshold, fewer exact tests)
+    RT2_VARIANT(348, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = kt_res_lean(false, false); x.kt_lane_w = true; return x; }()>, 1024, "mfmar/1024/kt4/res38/coop4/w4/cmp/dpp/lean/lw"),
+    RT2_VARIANT(349, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = kt_res_lean(false, false); x.kt_lane_w = true; x.exact_pf = true; return x; }()>, 1024, "mfmar/1024/kt4/res38/coop4/w4/cmp/dpp/lean/lw/xpf"),
+    RT2_VARIANT(350, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = kt_res_spec(4, true); x.lean = true; x.kt_lane_w = true; return x; }()>, 1024, "mfmar/1024/kt4/res38/coop4/w4/cmp/diag/dpp/lean/lw"),
     // ... on the LDS-tiled kernel (the form of 293): 19-group tiles at 3 waves per SIMD (schedules 1, 2), 16-group
     // tiles at 4 waves
     RT2_VARIANT(330, K_MFMA, render_mfma_k5t<kt_tiles_spec(19, 3, 1)>, 768, "mfmat5/768/kt1/tile19/coop0/w3/cmp/regs/perm"),
@@ -752,6 +756,8 @@ const Variant kVariants[] = {
     RT2_VARIANT(332, K_MFMA, render_mfma_k5t<kt_tiles_spec(19, 3, 4)>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm"),
     RT2_VARIANT(333, K_MFMA, render_mfma_k5t<kt_tiles_spec(16, 4, 1)>, 1024, "mfmat5/1024/kt1/tile16/coop0/w4/cmp/regs/perm"),
     RT2_VARIANT(335, K_MFMA, render_mfma_k5t<kt_tiles_spec(16, 4, 4)>, 1024, "mfmat5/1024/kt4/tile16/coop0/w4/cmp/regs/perm"),
+    RT2_VARIANT(351, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 4); x.kt_lane_w = true; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw"),
+    RT2_VARIANT(352, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 1); x.kt_lane_w = true; return x; }()>, 768, "mfmat5/768/kt1/tile19/coop0/w3/cmp/regs/perm/lw"),
     RT2_VARIANT(334, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 1); x.diag = true; return x; }()>, 768, "mfmat5/768/kt1/tile19/coop0/w3/cmp/regs/perm/diag"),
     RT2_VARIANT(299, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, true); x.fair_prio = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/fair/diag/dpp"),
     // earlier choices of rounds 3-4 (the 5-product form before and after the threshold moved into the accumulator,
@@ -1429,7 +1435,8 @@ extern "C" long long rt2_scene_export(rt2_scene* s, int what, void* host, unsign
 // (MfmaSpec::cthr: U, -V, X, Y shifted by TT = -Tl'', TT in the -tn slot),
 // 4 = layout 3 with the fragments built in registers by frag_pair (the
 // operand path of 282 / 293 / 298), 5 = the threshold in the K-slots
-// (MfmaSpec::kthr, frag_pair fragments: U, -V, X, Y, slot 3 zero).
+// (MfmaSpec::kthr, frag_pair fragments: U, -V, X, Y, slot 3 zero), 6 = layout
+// 5 with each ray's own W (MfmaSpec::kt_lane_w).
 // Host outputs, sized by the caller: terms [n_rays][n_pad][5]
 // (n_pad = triangles padded to 16 / 32), frags [n_rays][80] f16 bits (the LDS
 // row of layouts 0..3: main slots 0..31 and Y slots 16..31; layouts 4, 5 also
@@ -1438,7 +1445,7 @@ extern "C" long long rt2_scene_export(rt2_scene* s, int what, void* host, unsign
 extern "C" int rt2_mfma_probe(rt2_scene* s, int layout, const float* rays, int32_t n_rays, float* terms,
                               uint16_t* frags, float* rinfo, uint8_t* accept) {
     if (!s || !rays || n_rays <= 0 || n_rays % 64 != 0 || !terms || !frags || !rinfo || !accept ||
-        layout < 0 || layout > 5 || s->n_tris < 1 || !s->mfma_ok) {
+        layout < 0 || layout > 6 || s->n_tris < 1 || !s->mfma_ok) {
         rt2h::set_error("rt2_mfma_probe: bad argument (n_rays a positive multiple of 64, a scene in the filter's "
                         "range)");
         return -1;
@@ -1497,11 +1504,20 @@ extern "C" int rt2_mfma_probe(rt2_scene* s, int layout, const float* rays, int32
             x.perm_frag = true;
             return x;
         }();
+        constexpr MfmaSpec ktpl = [] {
+            MfmaSpec x = kt_res_spec(1);
+            x.perm_frag = true;
+            x.kt_lane_w = true;
+            return x;
+        }();
         if (layout == 4)
             hipLaunchKernelGGL(mfma_probe_kernel<k5cp>, dim3(n_rays / 64), dim3(64), 0, 0, p, d_rays, n_pad, d_terms,
                                d_frags, d_info, d_acc);
         else if (layout == 5)
             hipLaunchKernelGGL(mfma_probe_kernel<ktp>, dim3(n_rays / 64), dim3(64), 0, 0, p, d_rays, n_pad, d_terms,
+                               d_frags, d_info, d_acc);
+        else if (layout == 6)
+            hipLaunchKernelGGL(mfma_probe_kernel<ktpl>, dim3(n_rays / 64), dim3(64), 0, 0, p, d_rays, n_pad, d_terms,
                                d_frags, d_info, d_acc);
         else if (layout == 3)
             hipLaunchKernelGGL(mfma_probe_kernel<k5c>, dim3(n_rays / 64), dim3(64), 0, 0, p, d_rays, n_pad, d_terms,

@@ -261,18 +261,19 @@ def perm_fragments_match(frags, live):
     return int(a.sum() + y.sum())
 
 
-def kt_expected_fragments(frags, rinfo):
+def kt_expected_fragments(frags, rinfo, lane_w=False):
     """The kthr fragments (kt_frags / kt_y) recomputed on the host from the LDS
     row slots of the same rays: main K-half = d, m.x (hi lo hi), m.y hi, m.z
     hi, Tw', W'; Y = the row's Y slots with Tw' at slot 29.  Tw' = f16_up(Tw (1
-    + 2^-8)); W' = f16_up(W (1 + 2^-8)), W = the wave's largest mw_y + mw_z,
-    mw_c = max(|hi|, 2^11 |lo|) (float32 arithmetic as on the device)."""
+    + 2^-8)); W' = f16_up(W (1 + 2^-8)), W = the wave's largest mw_y + mw_z
+    (lane_w: the ray's own), mw_c = max(|hi|, 2^11 |lo|) (float32 arithmetic as
+    on the device)."""
     row = frags[:, :48].astype(np.float32)
     pad = np.float32(1.00390625)
     tw = f16_up(rinfo[:, 2].astype(np.float32) * pad)
     mw = (np.maximum(np.abs(row[:, 12]), np.float32(2048.0) * np.abs(row[:, 13])) +
           np.maximum(np.abs(row[:, 15]), np.float32(2048.0) * np.abs(row[:, 16]))).astype(np.float32)
-    W = np.repeat(mw.reshape(-1, 64).max(1), 64)
+    W = mw if lane_w else np.repeat(mw.reshape(-1, 64).max(1), 64)
     w16 = f16_up(W * pad)
     A = np.concatenate([row[:, 0:13], row[:, 15:16], tw[:, None], w16[:, None]], 1).astype(np.float64)
     Ay = row[:, 32:48].astype(np.float64).copy()
@@ -280,7 +281,7 @@ def kt_expected_fragments(frags, rinfo):
     return A, Ay, tw, w16
 
 
-def analyse_kt(terms, frags, rinfo, accept, Bkt, B16, T_tau):
+def analyse_kt(terms, frags, rinfo, accept, Bkt, B16, T_tau, lane_w=False):
     """One probe run of MfmaSpec::kthr (layout 5).  Checks: the records are the
     k16 records' slots with the threshold slots as specified (-tau; -B_q =
     -f16_up(2^-10 max over m.y, m.z of max(|hi|, 2^11 |lo|))); the register
@@ -300,7 +301,7 @@ def analyse_kt(terms, frags, rinfo, accept, Bkt, B16, T_tau):
     want_t = B16[:, 3, 16:32].copy()
     want_t[:, 13], want_t[:, 14], want_t[:, 15] = -tau, 0.0, 0.0
     rec_bad += int((Bkt[:, 3, :] != want_t).sum())
-    A_exp, Ay_exp, tw, w16 = kt_expected_fragments(frags, rinfo)
+    A_exp, Ay_exp, tw, w16 = kt_expected_fragments(frags, rinfo, lane_w)
     fr = frags.astype(np.float64)
     frag_bad = int((fr[live, 48:64] != A_exp[live]).sum() + (fr[live, 64:80] != Ay_exp[live]).sum())
     hw = terms[live][:, :n_tris, :].astype(np.float64)
@@ -321,7 +322,8 @@ def analyse_kt(terms, frags, rinfo, accept, Bkt, B16, T_tau):
     violations = np.argwhere(acc & ~passes)
     # how far the K-slot threshold reaches beyond the base threshold tau Tw
     base = tau[None, :] * rinfo[live, 2].astype(np.float64)[:, None]
-    grow = (-(A[:, None, 14] * Bkt[None, :, 0, 14]) - A[:, None, 15] * Bkt[None, :, :3, 15].max(-1)) / base
+    thr = -(A[:, None, None, 14] * Bkt[None, :, :3, 14] + A[:, None, None, 15] * Bkt[None, :, :3, 15])  # (R, T, q)
+    grow = thr.max(-1) / base
     out = {
         "rays_in_range": int(live.sum()), "pairs": int(acc.size), "accepted_pairs": int(acc.sum()),
         "filter_pass_frac": float(passes.mean()),

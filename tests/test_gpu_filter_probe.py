@@ -157,10 +157,12 @@ def test_filter_cthr_perm_on_hardware(rt2mod, torch_cuda, kind):
     assert st["acc_err_max_in_2^-24_sum_abs"] <= st["acc_err_bound_assumed"], st
 
 
+@pytest.mark.parametrize("layout", [5, 6], ids=["wave_w", "lane_w"])
 @pytest.mark.parametrize("kind", KINDS)
-def test_filter_kthr_on_hardware(rt2mod, torch_cuda, kind):
+def test_filter_kthr_on_hardware(rt2mod, torch_cuda, kind, layout):
     """MfmaSpec::kthr (the threshold in the K-slots) on the hardware, with the
-    shipping frag_pair operand path: the kt records and register fragments are
+    shipping frag_pair operand path, the B slot's ray factor W the wave's
+    maximum (layout 5) or each ray's own (layout 6, kt_lane_w): the kt records and register fragments are
     as specified, the terms are their 16 f16 products' exact sum within the
     assumed accumulation bound, and every reference-accepted pair passes."""
     rng = np.random.default_rng(300 + KINDS.index(kind))
@@ -169,9 +171,9 @@ def test_filter_kthr_on_hardware(rt2mod, torch_cuda, kind):
     B16 = fpl.records_k16(scene.export(3, np.uint16), len(V))
     Bkt = fpl.records_kt(scene.export(6, np.uint16), len(V))
     T_tau = scene.export(4, np.float32)
-    terms, frags, rinfo, accept = scene.mfma_probe(5, rays)
-    st, viol = fpl.analyse_kt(terms, frags, rinfo, accept, Bkt, B16, T_tau)
-    _results[f"{kind}/kthr"] = st
+    terms, frags, rinfo, accept = scene.mfma_probe(layout, rays)
+    st, viol = fpl.analyse_kt(terms, frags, rinfo, accept, Bkt, B16, T_tau, lane_w=layout == 6)
+    _results[f"{kind}/kthr" + ("_lane_w" if layout == 6 else "")] = st
     print(json.dumps(st, indent=1))
     assert st["record_slot_mismatches"] == 0 and st["fragment_slot_mismatches"] == 0, st
     assert st["rays_in_range"] >= len(rays) // 2 and st["accepted_pairs"] > 0
