@@ -251,10 +251,13 @@ int rt2_comm_check(rt2_comm* comm);
  * 16-byte pixels (an rgba32f image or the uint32x4 8-bit sums), device memory —
  * to `root` with one ncclGather and un-interleaves it there into d_image
  * (height*width pixels, device; ignored on other ranks).  shard.rank/nranks
- * must be the communicator's.  The ranks first agree that each of them can
- * take part (one agreement step on the communicator's own stream: the host
- * waits for it, not for `stream`); the gather and the un-interleave are then
- * asynchronous on `stream`.  A local failure (a root without d_image, a
+ * must be the communicator's.  The host first waits for the work already
+ * queued on `stream` (this rank's render: no peer is involved, so no deadline
+ * applies; bounded at 20 x RT2_COMM_TIMEOUT_S, and twice its duration is added
+ * to the deadlines that follow), then the ranks agree that each of them can
+ * take part (one agreement step on the communicator's own stream, which could
+ * not start on a device still busy with the render); the gather and the
+ * un-interleave are then asynchronous on `stream`.  A local failure (a root without d_image, a
  * shard that does not match, no device memory) makes every rank return < 0
  * with nothing issued.  Once the gather is queued, a peer that fails inside
  * it (ncclCommAbort does not release ranks already in the collective) leaves
@@ -268,9 +271,8 @@ int rt2_gather_slabs(rt2_comm* comm, const void* d_slab, int32_t width, int32_t 
  * aborted as above and < 0 returned (replaces the caller's
  * hipStreamSynchronize / cudaStreamSynchronize after the collective).  When
  * the last rt2_gather_slabs of this communicator was queued on `stream`, the
- * work queued before that gather (this rank's render: no peer is involved) is
- * waited for first, outside the deadline (bounded at 20 x the timeout), and
- * twice its duration is added to the deadline of the gather itself. */
+ * work queued before that gather (already waited for by rt2_gather_slabs) is
+ * excluded from the deadline in the same way. */
 int rt2_comm_wait(rt2_comm* comm, void* stream);
 /* The root's un-interleave alone: d_gathered = [nranks][max_rows][width]
  * 16-byte pixels (rank-major slabs, padded to max_rows rows) -> d_image

@@ -437,6 +437,24 @@ extern "C" int rt2_gather_slabs(rt2_comm* c, const void* d_slab, int32_t width, 
         return 0;
     };
     RcclTransport t{c};
+    // The rank's own work already queued on `stream` (its render) is waited
+    // for first, without the collective's deadline (bounded at 20x it), and
+    // twice its duration becomes slack on the deadlines that follow: the
+    // agreement's allreduce cannot start on a device still busy with the
+    // render, so a render longer than RT2_COMM_TIMEOUT_S would otherwise
+    // abort a healthy job at the agreement
+    if (hipSetDevice(c->device) != hipSuccess) {
+        rt2h::set_error("rt2_gather_slabs: hipSetDevice failed");
+        return -1;
+    }
+    if (!c->aborted && c->comm) {
+        if ((!c->pre_gather && hipEventCreateWithFlags(&c->pre_gather, hipEventDisableTiming) != hipSuccess) ||
+            hipEventRecord(c->pre_gather, st) != hipSuccess) {
+            rt2h::set_error("rt2_gather_slabs: could not record the render's event");
+            return -1;
+        }
+        if (t.wait_local_event(c->pre_gather) != 0) return -1;  // aborted, error set
+    }
     std::string err;
     if (rt2p::gather_slabs(t, prepare, gather, finish, err) != 0) {
         rt2h::set_error("rt2_gather_slabs: " + err);

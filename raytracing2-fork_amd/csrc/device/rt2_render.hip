@@ -656,10 +656,11 @@ constexpr MfmaSpec kt_tiles_spec(int K, int waves, int sched) {
     return x;
 }
 // the round-6 defaults: kthr 4, the lean lane state; l2 = the L2 continuation (39..256 groups), fair = rank slabs
-constexpr MfmaSpec kt_res_lean(bool l2, bool fair) {
+constexpr MfmaSpec kt_res_lean(bool l2, bool fair, bool lane_w = false) {
     MfmaSpec x = kt_res_spec(4, false, l2);
     x.lean = true;
     x.fair_prio = fair;
+    x.kt_lane_w = lane_w;
     return x;
 }
 constexpr int kResL2Groups = 256;  // render_mfma_k5r with res_l2: 38 groups resident, the rest from L2
@@ -690,15 +691,21 @@ const Variant kVariants[] = {
     // records in LDS for the whole launch, 38 groups, the rest read from L2) with the threshold in the K-slots
     // (MfmaSpec::kthr 4: 8 independent products per group, the two 32-ray blocks interleaved; DESIGN.md "The
     // threshold in the K-slots"), the lean lane state; fair-share issue priority for rank slabs
+    RT2_VARIANT(353, K_MFMA, render_mfma_k5r<kt_res_lean(false, false, true)>, 1024, "mfmar/1024/kt4/res38/coop4/w4/cmp/dpp/lean/lw"),
+    RT2_VARIANT(354, K_MFMA, render_mfma_k5r<kt_res_lean(false, true, true)>, 1024, "mfmar/1024/kt4/res38/coop4/w4/cmp/fair/dpp/lean/lw"),
+    RT2_VARIANT(355, K_MFMA, render_mfma_k5r<kt_res_lean(true, false, true)>, 1024, "mfmarl2/1024/kt4/res38l2/coop4/w4/cmp/dpp/lean/lw"),
+    RT2_VARIANT(356, K_MFMA, render_mfma_k5r<kt_res_lean(true, true, true)>, 1024, "mfmarl2/1024/kt4/res38l2/coop4/w4/cmp/fair/dpp/lean/lw"),
+    // the default above 8,192 triangles: the LDS-tiled kernel (rt2_k5_tiles.h; 19-group tiles, fragments in
+    // registers) with the threshold in the K-slots, each ray's own W in the bound (round 6; round 5: 293)
+    RT2_VARIANT(351, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 4); x.kt_lane_w = true; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw"),
+#ifdef RT2_EXPERIMENTS
+    // round 6's first kthr defaults (the wave's W in the bound; 353-356 take each ray's own)
     RT2_VARIANT(342, K_MFMA, render_mfma_k5r<kt_res_lean(false, false)>, 1024, "mfmar/1024/kt4/res38/coop4/w4/cmp/dpp/lean"),
     RT2_VARIANT(344, K_MFMA, render_mfma_k5r<kt_res_lean(false, true)>, 1024, "mfmar/1024/kt4/res38/coop4/w4/cmp/fair/dpp/lean"),
     RT2_VARIANT(345, K_MFMA, render_mfma_k5r<kt_res_lean(true, false)>, 1024, "mfmarl2/1024/kt4/res38l2/coop4/w4/cmp/dpp/lean"),
     RT2_VARIANT(346, K_MFMA, render_mfma_k5r<kt_res_lean(true, true)>, 1024, "mfmarl2/1024/kt4/res38l2/coop4/w4/cmp/fair/dpp/lean"),
-    // the default above 8,192 triangles (round 5): 217 with the fragments built in registers (no LDS rows), so the
-    // tiles hold 19 groups
+    // the defaults of rounds 4-5 (round 6 replaced them by the kthr resident kernels 353-356 and the kthr tiles 351)
     RT2_VARIANT(293, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = k5_tiles_spec(19, true, 0); x.rows80 = true; x.lane_lds = 0; x.cthr = true; x.perm_frag = true; return x; }()>, 768, "mfmat5/768/k5/notn/tile19/coop0/w3/cmp/regs/cthr/perm"),
-#ifdef RT2_EXPERIMENTS
-    // the defaults of rounds 4-5 (round 6 replaced them by the kthr resident kernels 342-346)
     // (round 4) scenes of <= 8,192 triangles (records L2-resident): the same without the -tn term (4 products per block) and
     // with the threshold in the products' accumulator (MfmaSpec::cthr, DESIGN.md "The threshold in the
     // accumulator"), 4 waves (packed path state, Y fragments read per block: 263), or 3 when the packed fields do not
@@ -756,7 +763,6 @@ const Variant kVariants[] = {
     RT2_VARIANT(332, K_MFMA, render_mfma_k5t<kt_tiles_spec(19, 3, 4)>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm"),
     RT2_VARIANT(333, K_MFMA, render_mfma_k5t<kt_tiles_spec(16, 4, 1)>, 1024, "mfmat5/1024/kt1/tile16/coop0/w4/cmp/regs/perm"),
     RT2_VARIANT(335, K_MFMA, render_mfma_k5t<kt_tiles_spec(16, 4, 4)>, 1024, "mfmat5/1024/kt4/tile16/coop0/w4/cmp/regs/perm"),
-    RT2_VARIANT(351, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 4); x.kt_lane_w = true; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw"),
     RT2_VARIANT(352, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 1); x.kt_lane_w = true; return x; }()>, 768, "mfmat5/768/kt1/tile19/coop0/w3/cmp/regs/perm/lw"),
     RT2_VARIANT(334, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 1); x.diag = true; return x; }()>, 768, "mfmat5/768/kt1/tile19/coop0/w3/cmp/regs/perm/diag"),
     RT2_VARIANT(299, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, true); x.fair_prio = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/fair/diag/dpp"),
@@ -812,25 +818,22 @@ constexpr int kDefaultBvh = 109;
 constexpr int kLargeScene = 86;  // tiled/512/max3f4: LDS tiles above kSmemMaxTris triangles
 constexpr int kSlab = 92;        // assist12/max3f8/w6: fewer than 4 items per lane (multi-GPU slabs)
 constexpr int kMfmaSlabMaxTris = 8192;  // = kResL2Groups x 32: the resident kernel with its L2 continuation
-constexpr int kMfmaRes = 342;      // <= kResGroups groups (config B): every record resident in LDS, 4 waves per SIMD,
-                                   // the threshold in the K-slots (kthr 4), the lean lane state (rt2_k5_resident.h;
-                                   // DESIGN.md "The threshold in the K-slots"): config B 146.9-149.4 vs 154.2-165.3 ms
-                                   // for round 5's 282 in A/Bs on two boxes, identical image
-constexpr int kMfmaResSlab = 344;  // ... launches with < kResSlabItems items per resident lane (rank slabs): the
+constexpr int kMfmaRes = 353;      // <= kResGroups groups (config B): every record resident in LDS, 4 waves per SIMD,
+                                   // the threshold in the K-slots (kthr 4, each ray's own W in the bound), the lean
+                                   // lane state (rt2_k5_resident.h; DESIGN.md "The threshold in the K-slots"): config
+                                   // B 149.0 vs 152.8 ms (342, the wave's W) vs 154.2-165.3 ms for round 5's 282 in
+                                   // A/Bs, identical images
+constexpr int kMfmaResSlab = 354;  // ... launches with < kResSlabItems items per resident lane (rank slabs): the
                                    // same kernel with fair-share issue priority (MfmaSpec::fair_prio; round 5: 298)
 constexpr unsigned long long kResSlabItems = 6;
-constexpr int kMfmaResL2 = 345;    // 39..256 groups (configs W, K): 38 groups resident, the rest read from L2
+constexpr int kMfmaResL2 = 355;    // 39..256 groups (configs W, K): 38 groups resident, the rest read from L2
                                    // (MfmaSpec::res_l2): config W 28.7 vs 46.5 ms, K 306.8 vs 362.1 ms for round 4-5's
-                                   // L2-resident 263 (A/B, identical images)
-constexpr int kMfmaResL2Slab = 346;  // ... its rank slabs (fair-share priority)
-constexpr int kMfmaTiles = 293;    // larger scenes (round 5): 217's LDS tiles with the fragments built in registers
-                                   // (v_permlane32_swap, no LDS rows), so the tiles grow to 19 groups: config C
-                                   // 23.63 vs 23.87 s, config E 6.14 vs 6.23 s (same images); round 4's 217:
-                                   // the 5-product form without -tn with workgroup-shared LDS record tiles of 10
-                                   // groups, the path state in registers (rt2_k5_tiles.h; DESIGN.md "LDS record
-                                   // tiles"), the threshold in the accumulator.  The kthr form does not pay here
-                                   // (C sample 1,049 vs 1,049 ms, E 1,228 vs 1,206 ms: DESIGN.md "The threshold in
-                                   // the K-slots")
+                                   // L2-resident 263 (A/B of the wave-W form 337, identical images)
+constexpr int kMfmaResL2Slab = 356;  // ... its rank slabs (fair-share priority)
+constexpr int kMfmaTiles = 351;    // larger scenes: the LDS-tiled kernel (rt2_k5_tiles.h: one 12-wave workgroup per
+                                   // CU, 19-group record tiles, fragments in registers) with the threshold in the
+                                   // K-slots and each ray's own W: config C sample 962 vs 1,076 ms, config E sample
+                                   // 1,081 vs 1,230 ms for round 5's 293 (cthr; A/B, identical images)
 constexpr int kMfma = 227;  // mfma/.../k5/...: the matrix-core filter on v_mfma_f32_32x32x16_f16, 5 products per
                             // 32-ray block (DESIGN.md "The 5-product form"), registers only; larger scenes whose
                             // packed path state cannot hold the launch

@@ -133,7 +133,7 @@ def test_filter_cthr_on_hardware(rt2mod, torch_cuda, kind):
 
 @pytest.mark.parametrize("kind", KINDS)
 def test_filter_cthr_perm_on_hardware(rt2mod, torch_cuda, kind):
-    """The operand path the cthr kernels (293; round 5's 282 / 298) use: the
+    """The operand path the cthr kernels (round 5's 293 / 282 / 298) use: the
     fragments built in registers by frag_pair (v_permlane32_swap), not read
     from LDS rows.  The MFMA must see exactly the row's slots, and the layout-3
     checks (TT, accumulation, conservativeness) must hold on those terms."""
@@ -239,8 +239,9 @@ def near_threshold_scene(rt2mod):
     return sd
 
 
-@pytest.mark.parametrize("variant", [227, 293, 342, 344, 345, 346, 228, 231, 233, 212, 213, 217, 260, 261, 262, 263, 243, 250,
-                                     252, 280, 282, 298, 320, 321, 322, 323, 325, 326, 329, 330, 332, 336, 337, 340])
+@pytest.mark.parametrize("variant", [227, 351, 353, 354, 355, 356, 293, 342, 344, 345, 346, 228, 231, 233, 212, 213, 217, 260, 261, 262, 263, 243, 250,
+                                     252, 280, 282, 298, 320, 321, 322, 323, 325, 326, 329, 330, 332, 336, 337, 340,
+                                     347, 348, 349, 350, 352])
 def test_near_threshold_scene_bit_exact(rt2mod, oraclemod, torch_cuda, variant):
     if not rt2mod.has_variant(variant):
         pytest.skip(f"variant {variant} not in this build")
