@@ -308,6 +308,239 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, SH& sh,
     return in_range;
 }
 
+// MfmaSpec::tile_flow — the record tiles as a stream with LDS counters instead
+// of a workgroup barrier per tile (round 6; DESIGN.md "LDS record tiles").
+// With one barrier per tile the 12 waves meet 165 times per config C segment,
+// and every meeting drains the SIMDs: the wave that falls behind (age priority,
+// its exact tests) finishes its tile alone while the others wait — 25-33 % of
+// wave cycles in the round-5 phase clocks.  Here a wave waits only for the
+// tile it is about to read, so the waves of a SIMD stay staggered (up to one
+// tile apart with two buffers) and the per-tile drain goes away.
+//
+// Every wave walks the same stream of tiles (stream index s: tile s % nt of
+// the segment, buffer s % NB; a segment is nt consecutive indices, so the
+// index runs on across segments) and, per tile: waits until landed[b] says
+// tile s is in buffer b, sweeps it (when it has rays), and releases it
+// (rel[b] += 1).  Tile s may be issued once every wave has released tile
+// s - NB (rel[b] == NW * (s / NB)); the first wave to find it issuable claims
+// it (compare-and-swap on `issued`), issues all its LDS-DMA pieces itself,
+// and publishes landed[b] = s + 1 after its own `s_waitcnt vmcnt(0)` — at the
+// start of its next tile, or at once when it is waiting anyway.  Claims are
+// tried in the middle of a tile (the claimer is then a wave that runs ahead)
+// and in the wait loop (so a tile that nobody has claimed yet cannot stall
+// the stream).  No wave reads a buffer before its tile's claimer has seen the
+// DMA land, and no DMA overwrites a buffer before all NW waves released it.
+template <int NB>
+struct TileFlow {
+    uint32_t issued;      // stream indices claimed so far (the next one to issue)
+    uint32_t landed[NB];  // per buffer: 1 + the stream index of the tile whose pieces have all landed there
+    uint32_t rel[NB];     // per buffer: releases so far (NW per tile)
+};
+// the wave's place in the stream (wave-uniform; kept across segments)
+struct FlowWave {
+    uint32_t next = 0;  // stream index of the next tile this wave reads
+    int pend = -1;      // a tile this wave claimed (tile_flow 2: its share) whose landing it has not published yet
+    uint32_t next_issue = 0;  // tile_flow 2: the next tile this wave issues its share of
+    int age = 0;              // tile_flow 2: groups swept since the pending share was issued
+};
+
+__device__ __forceinline__ uint32_t lds_acquire(uint32_t* a) {
+    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(a, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+
+template <MfmaSpec S, class TL, class FL>
+__device__ __forceinline__ bool sweep_kt_flow(const RenderParams& p, TL& tl, FL& fl, FlowWave& fw, const f3& o,
+                                              const f3& d, float& best, int& bi, float& bestK, MfmaDiag& dg,
+                                              bool sweeping, bool upper) {
+    static_assert(S.kthr && S.perm_frag && S.tile_groups > 0, "the kthr form with register fragments");
+    constexpr int K = S.tile_groups, NW = S.block / 64, NB = S.tile_bufs;
+    const int lane = (int)lane_id();
+    // MfmaSpec::diag: shader clocks per phase (MfmaDiag t_wait / t_filt / t_exact / t_swp)
+    [[maybe_unused]] unsigned long long tc = 0, tsw = 0;
+    if constexpr (S.diag) tsw = tc = __builtin_amdgcn_s_memtime();
+    auto stamp = [&](unsigned long long& acc) {
+        if constexpr (S.diag) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            acc += t - tc;
+            tc = t;
+        }
+    };
+    MfmaScale sc{0.0f, 0.0f, 0.0f};
+    h8 a0[2], y1[2];
+    _Float16 tw16 = (_Float16)0.0f;
+    bool compute = false, in_range = true;
+    if (sweeping) {
+        const f3 m = cross(d, o);
+        in_range = mfma_scale<S>(p.mfma_A, o, d, m, sc);
+        if (in_range) {
+            kt_frags<S>(d, m, sc, a0, tw16);
+            kt_y(d, o, bestK, sc, tw16, y1);
+            compute = true;
+        }
+    }
+    const int ng = (p.n_tris + 31) >> 5, nt = (ng + K - 1) / K;
+    const h8* gsrc = reinterpret_cast<const h8*>(p.mfma_kt_frag) + lane;
+    // every LDS-DMA piece of stream index s (4 per group, 1 KiB each: a lane's
+    // 16 B land at base + 16 lane); the kt records of a tile are contiguous
+    auto issue_tile = [&](uint32_t s) {
+        const int g0 = (int)(s % (uint32_t)nt) * K, gn = min(K, ng - g0), b = (int)(s % NB);
+        const h8* src = gsrc + (size_t)g0 * (kKtOps * 64);
+        for (int pc = 0; pc < kKtOps * gn; pc++)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + pc * 64),
+                                             (__attribute__((address_space(3))) void*)&tl.rec[b][pc * 64], 16, 0, 0);
+    };
+    // tile_flow 2: every wave issues its own share of each tile's pieces
+    // (round-robin, pc = wave, wave + NW, ...: no wave pays a whole tile's
+    // LDS-DMA issue) and publishes it by landed[b] += 1; a tile is in its
+    // buffer when all NW shares are (landed[b] == NW * (s / NB + 1))
+    const int wave = (int)(threadIdx.x >> 6);
+    auto issue_share = [&](uint32_t s) {
+        const int g0 = (int)(s % (uint32_t)nt) * K, gn = min(K, ng - g0), b = (int)(s % NB);
+        const h8* src = gsrc + (size_t)g0 * (kKtOps * 64);
+        for (int pc = wave; pc < kKtOps * gn; pc += NW)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + pc * 64),
+                                             (__attribute__((address_space(3))) void*)&tl.rec[b][pc * 64], 16, 0, 0);
+    };
+    auto publish_share = [&]() {
+        [[maybe_unused]] unsigned long long t0 = 0;
+        if constexpr (S.diag) t0 = __builtin_amdgcn_s_memtime();
+        wait_vm0();
+        if constexpr (S.diag) dg.t_pub += __builtin_amdgcn_s_memtime() - t0;
+        if (lane == 0) __hip_atomic_fetch_add(&fl.landed[fw.pend % NB], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        fw.pend = -1;
+    };
+    // the wave's part of the stream's upkeep: publish a share that has had
+    // time to land (`force`: now), then issue the next share once every wave
+    // has released that tile's buffer
+    auto upkeep = [&](bool force, bool try_issue) {
+        if (fw.pend >= 0 && (force || fw.age >= 2)) publish_share();
+        if (fw.pend < 0 && try_issue) {
+            const uint32_t s = fw.next_issue;
+            if (lds_acquire(&fl.rel[s % NB]) == (uint32_t)NW * (s / NB)) {
+                [[maybe_unused]] unsigned long long t0 = 0;
+                if constexpr (S.diag) t0 = __builtin_amdgcn_s_memtime();
+                issue_share(s);
+                if constexpr (S.diag) {
+                    dg.t_issue += __builtin_amdgcn_s_memtime() - t0;
+                    dg.claims += 1;
+                }
+                fw.pend = (int)s;
+                fw.age = 0;
+                fw.next_issue = s + 1u;
+            }
+        }
+    };
+    auto publish = [&]() {
+        if (fw.pend < 0) return;
+        [[maybe_unused]] unsigned long long t0 = 0;
+        if constexpr (S.diag) t0 = __builtin_amdgcn_s_memtime();
+        wait_vm0();  // this wave's pieces (the only vector-memory operations it has in flight) have landed
+        if constexpr (S.diag) dg.t_pub += __builtin_amdgcn_s_memtime() - t0;
+        if (lane == 0)
+            __hip_atomic_store(&fl.landed[fw.pend % NB], (uint32_t)fw.pend + 1u, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        fw.pend = -1;
+    };
+    auto try_claim = [&]() {
+        uint32_t s = lds_acquire(&fl.issued);
+        const uint32_t b = s % NB;
+        if (lds_acquire(&fl.rel[b]) != (uint32_t)NW * (s / NB)) return;  // a wave still reads tile s - NB
+        uint32_t won = 0;
+        if (lane == 0)
+            won = __hip_atomic_compare_exchange_strong(&fl.issued, &s, s + 1u, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
+                                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (!__builtin_amdgcn_readfirstlane(won)) return;
+        s = __builtin_amdgcn_readfirstlane(s);
+        [[maybe_unused]] unsigned long long t0 = 0;
+        if constexpr (S.diag) t0 = __builtin_amdgcn_s_memtime();
+        issue_tile(s);
+        if constexpr (S.diag) {
+            dg.t_issue += __builtin_amdgcn_s_memtime() - t0;
+            dg.claims += 1;
+        }
+        fw.pend = (int)s;
+    };
+    for (int t = 0; t < nt; t++) {
+        const uint32_t s = fw.next++;
+        const int b = (int)(s % NB), gn = min(K, ng - t * K);
+        stamp(dg.t_exact);
+        if constexpr (S.tile_flow == 2) {
+            upkeep(true, true);
+            while (lds_acquire(&fl.landed[b]) < (uint32_t)NW * (s / NB + 1u)) {
+                upkeep(true, true);
+                __builtin_amdgcn_s_sleep(1);
+            }
+        } else {
+            publish();  // a tile claimed during the previous one: its DMA had half a tile to land
+            while (lds_acquire(&fl.landed[b]) < s + 1u) {
+                if (fw.pend >= 0)
+                    publish();
+                else
+                    try_claim();
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        stamp(dg.t_wait);
+        if (S.tile_flow == 1 && S.flow_early && fw.pend < 0) try_claim();  // MfmaSpec::flow_early: a full tile of lead
+        if (compute) {
+            const h8* tb = &tl.rec[b][lane];
+            for (int gi = 0; gi < gn; gi++) {
+                const int G = t * K + gi;
+                const h8 b0 = tb[0], b1 = tb[64], b2 = tb[128], b3 = tb[192];
+                tb += kKtOps * 64;
+                if constexpr (S.tile_flow == 2) {
+                    fw.age++;
+                    upkeep(false, gi == K / 2);
+                } else if (gi == K / 2 && fw.pend < 0) {
+                    try_claim();
+                }
+                const unsigned long long M = kt_group<S>(a0, y1, b0, b1, b2, b3, upper);
+                if constexpr (S.diag) dg.groups += 1;
+                stamp(dg.t_filt);
+                if (M) {
+                    if constexpr (S.diag) dg.hot += 1;
+                    // the exact phase, in index order (compute.glsl:302-340, strict `dst < best`)
+                    uint32_t m32 = (uint32_t)(M | M >> 32);
+                    const float bk0 = bestK;
+                    while (m32) {
+                        const int idx = 32 * G + __builtin_ctz(m32);
+                        m32 &= m32 - 1;
+                        if (idx >= p.n_tris) break;
+                        if constexpr (S.diag) dg.exact += 1;
+                        cfloat* tp = (cfloat*)p.tri + 12 * idx;
+                        const MtQ qq = mt_quantities(o, d, ldc4(tp), ldc4(tp + 4), ldc4(tp + 8));
+                        if (mt_pass3(qq, bestK)) mt_exact(qq, idx, best, bi, bestK);
+                    }
+                    if (__ballot(bestK != bk0)) kt_y(d, o, bestK, sc, tw16, y1);
+                    stamp(dg.t_exact);
+                }
+            }
+        }
+        // done with buffer b (the LDS executes this wave's reads before the add)
+        uint32_t r_old = 0;
+        if (lane == 0) r_old = __hip_atomic_fetch_add(&fl.rel[b], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if constexpr (S.flow_prio) {
+            // MfmaSpec::flow_prio: issue priority for the next tile by this
+            // wave's place among the NW that finished this one (the last ones
+            // are behind: they take the SIMD's issue slots first)
+            const int rank = (int)(__builtin_amdgcn_readfirstlane(r_old) - (uint32_t)NW * (s / NB));
+            const int q = rank * 4 / NW;
+            if (q >= 3)
+                __builtin_amdgcn_s_setprio(3);
+            else if (q == 2)
+                __builtin_amdgcn_s_setprio(2);
+            else if (q == 1)
+                __builtin_amdgcn_s_setprio(1);
+            else
+                __builtin_amdgcn_s_setprio(0);
+        }
+    }
+    if constexpr (S.flow_prio) __builtin_amdgcn_s_setprio(0);
+    stamp(dg.t_exact);
+    if constexpr (S.diag) dg.t_swp += __builtin_amdgcn_s_memtime() - tsw;
+    return in_range;
+}
+
 // render_mfma's lockstep segment loop around sweep_k5_tiles: every wave of the
 // workgroup takes part in every tile barrier of every segment the workgroup
 // runs (block_any decides, workgroup-uniformly, whether it runs one), sweeping
@@ -328,11 +561,24 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
     __shared__ WL wl[S.perm_frag ? 1 : NW];
     __shared__ K5Tiles<S.tile_groups, S.tile_bufs, !(S.cthr || S.kthr)> tl;
     __shared__ BlockVote<NW> vote;
+    // MfmaSpec::tile_flow: the tile stream's counters (sweep_kt_flow)
+    __shared__ TileFlow<S.tile_bufs> flow;
+    FlowWave fw;
+    if constexpr (S.tile_flow) {
+        static_assert(S.tile_flow == 1 || S.tile_flow == 2, "tile_flow 1 (claims) or 2 (shares)");
+        if (threadIdx.x == 0) {
+            flow.issued = 0;
+            for (int b = 0; b < S.tile_bufs; b++) flow.landed[b] = flow.rel[b] = 0;
+        }
+        __syncthreads();
+    }
     uint32_t vote_parity = 0;
     WL& sh = wl[S.perm_frag ? 0 : threadIdx.x >> 6];
     Lane L;
     lane_init(L);
     MfmaDiag dg;
+    [[maybe_unused]] unsigned long long t_start = 0;
+    if constexpr (S.diag) t_start = __builtin_amdgcn_s_memtime();
     for (;;) {
         const RenderParams& p = kargs<RenderParams>();
         advance(L, p);
@@ -372,7 +618,11 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
             lane_stash_packed(L, sh.lane, (int)lane_id());
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         }
-        const bool swept = sweep_k5_tiles<S>(p, sh, tl, ro, rd, best, bi, bestK, dg, sweeping, upper);
+        bool swept;
+        if constexpr (S.tile_flow)
+            swept = sweep_kt_flow<S>(p, tl, flow, fw, ro, rd, best, bi, bestK, dg, sweeping, upper);
+        else
+            swept = sweep_k5_tiles<S>(p, sh, tl, ro, rd, best, bi, bestK, dg, sweeping, upper);
         if constexpr (stash) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             lane_unstash_packed(L, sh.lane, (int)lane_id());
@@ -398,6 +648,9 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
             shade(L, p, best, bi);
         }
     }
+    // tile_flow: a claim of the next segment's first tile may still be in
+    // flight; it must land before the workgroup's LDS is given back
+    if constexpr (S.tile_flow) wait_vm0();
     const RenderParams& p = kargs<RenderParams>();
     flush_counters(L, p);
     if constexpr (S.diag)
@@ -405,6 +658,16 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
             atomicAdd(p.seg_counter + 1, dg.groups);  // (wave, triangle group) sweeps
             atomicAdd(p.seg_counter + 2, dg.hot);     // ... with a passing pair
             atomicAdd(p.seg_counter + 3, dg.exact);   // (wave, triangle) exact tests
+            if constexpr (S.tile_flow) {
+                atomicAdd(p.seg_counter + 12, dg.t_wait);  // shader clocks: waiting for tiles
+                atomicAdd(p.seg_counter + 13, dg.t_filt);  // ... products + record reads
+                atomicAdd(p.seg_counter + 14, dg.t_exact); // ... exact phase + Y rebuilds (+ loop)
+                atomicAdd(p.seg_counter + 15, dg.t_swp);   // ... whole sweeps
+                atomicAdd(p.seg_counter + 16, __builtin_amdgcn_s_memtime() - t_start);  // ... the wave's life
+                atomicAdd(p.seg_counter + 17, dg.t_issue);  // ... issuing claimed tiles (inside wait / filter)
+                atomicAdd(p.seg_counter + 18, dg.t_pub);    // ... a claimer's wait for its pieces (inside wait)
+                atomicAdd(p.seg_counter + 19, dg.claims);   // tiles claimed
+            }
         }
 }
 

@@ -763,6 +763,20 @@ const Variant kVariants[] = {
     RT2_VARIANT(332, K_MFMA, render_mfma_k5t<kt_tiles_spec(19, 3, 4)>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm"),
     RT2_VARIANT(333, K_MFMA, render_mfma_k5t<kt_tiles_spec(16, 4, 1)>, 1024, "mfmat5/1024/kt1/tile16/coop0/w4/cmp/regs/perm"),
     RT2_VARIANT(335, K_MFMA, render_mfma_k5t<kt_tiles_spec(16, 4, 4)>, 1024, "mfmat5/1024/kt4/tile16/coop0/w4/cmp/regs/perm"),
+    // ... the tiles as a stream with LDS counters (MfmaSpec::tile_flow: no barrier per tile), 2 x 19 or 3 x 12 groups
+    RT2_VARIANT(357, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 4); x.kt_lane_w = true; x.tile_flow = 1; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flow"),
+    RT2_VARIANT(358, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(12, 3, 4); x.kt_lane_w = true; x.tile_flow = 1; x.tile_bufs = 3; return x; }()>, 768, "mfmat5/768/kt4/tile12x3/coop0/w3/cmp/regs/perm/lw/flow"),
+    RT2_VARIANT(359, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 4); x.kt_lane_w = true; x.tile_flow = 1; x.diag = true; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flow/diag"),
+    RT2_VARIANT(360, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 4); x.kt_lane_w = true; x.tile_flow = 1; x.flow_early = true; x.diag = true; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flowe/diag"),
+    RT2_VARIANT(361, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(9, 3, 4); x.kt_lane_w = true; x.tile_flow = 1; x.flow_early = true; x.tile_bufs = 4; x.diag = true; return x; }()>, 768, "mfmat5/768/kt4/tile9x4/coop0/w3/cmp/regs/perm/lw/flowe/diag"),
+    RT2_VARIANT(362, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(12, 3, 4); x.kt_lane_w = true; x.tile_flow = 1; x.flow_early = true; x.tile_bufs = 3; x.diag = true; return x; }()>, 768, "mfmat5/768/kt4/tile12x3/coop0/w3/cmp/regs/perm/lw/flowe/diag"),
+    RT2_VARIANT(363, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 4); x.kt_lane_w = true; x.tile_flow = 1; x.flow_prio = true; x.diag = true; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flowp/diag"),
+    RT2_VARIANT(364, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 4); x.kt_lane_w = true; x.tile_flow = 1; x.flow_prio = true; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flowp"),
+    RT2_VARIANT(365, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(9, 3, 4); x.kt_lane_w = true; x.tile_flow = 1; x.flow_prio = true; x.tile_bufs = 4; x.diag = true; return x; }()>, 768, "mfmat5/768/kt4/tile9x4/coop0/w3/cmp/regs/perm/lw/flowp/diag"),
+    RT2_VARIANT(366, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 4); x.kt_lane_w = true; x.tile_flow = 2; x.diag = true; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flow2/diag"),
+    RT2_VARIANT(367, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(12, 3, 4); x.kt_lane_w = true; x.tile_flow = 2; x.tile_bufs = 3; x.diag = true; return x; }()>, 768, "mfmat5/768/kt4/tile12x3/coop0/w3/cmp/regs/perm/lw/flow2/diag"),
+    RT2_VARIANT(368, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 4); x.kt_lane_w = true; x.tile_flow = 2; x.flow_prio = true; x.diag = true; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flow2p/diag"),
+    RT2_VARIANT(369, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 4); x.kt_lane_w = true; x.tile_flow = 2; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flow2"),
     RT2_VARIANT(352, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 1); x.kt_lane_w = true; return x; }()>, 768, "mfmat5/768/kt1/tile19/coop0/w3/cmp/regs/perm/lw"),
     RT2_VARIANT(334, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 1); x.diag = true; return x; }()>, 768, "mfmat5/768/kt1/tile19/coop0/w3/cmp/regs/perm/diag"),
     RT2_VARIANT(299, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, true); x.fair_prio = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/fair/diag/dpp"),

@@ -82,6 +82,16 @@ for rnd in range(a.rounds):
                 diag[v]["clock_share"] = dict(zip(("advance", "sweep", "shade", "tail"),
                                                   [round(x / sum(tt), 4) for x in tt]))
                 diag[v]["sweep_clocks_per_group"] = round(c[10] / c[2], 1)
+            tf = [c[13], c[14], c[15], c[16], c[17]]  # render_mfma_k5t tile_flow diag: wait, filter, exact, sweep, life
+            if tf[4]:
+                diag[v]["flow_clock_share"] = dict(
+                    wait=round(tf[0] / tf[4], 4), filter=round(tf[1] / tf[4], 4), exact=round(tf[2] / tf[4], 4),
+                    sweep=round(tf[3] / tf[4], 4), outside_sweep=round(1 - tf[3] / tf[4], 4))
+                diag[v]["filter_clocks_per_group"] = round(tf[1] / c[2], 1)
+                diag[v]["flow_clock_share"].update(issue=round(c[18] / tf[4], 4), claimer_wait=round(c[19] / tf[4], 4))
+                diag[v]["claims"] = c[20]
+                diag[v]["issue_clocks_per_claim"] = round(c[18] / max(c[20], 1), 1)
+                diag[v]["claimer_wait_clocks_per_claim"] = round(c[19] / max(c[20], 1), 1)
         if rnd == 0:
             if ref is None:
                 ref = img
