@@ -777,6 +777,7 @@ const Variant kVariants[] = {
     RT2_VARIANT(367, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(12, 3, 4); x.kt_lane_w = true; x.tile_flow = 2; x.tile_bufs = 3; x.diag = true; return x; }()>, 768, "mfmat5/768/kt4/tile12x3/coop0/w3/cmp/regs/perm/lw/flow2/diag"),
     RT2_VARIANT(368, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 4); x.kt_lane_w = true; x.tile_flow = 2; x.flow_prio = true; x.diag = true; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flow2p/diag"),
     RT2_VARIANT(369, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 4); x.kt_lane_w = true; x.tile_flow = 2; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flow2"),
+    RT2_VARIANT(370, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 4); x.kt_lane_w = true; x.tile_flow = 2; x.flow_prio = true; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flow2p"),
     RT2_VARIANT(352, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 1); x.kt_lane_w = true; return x; }()>, 768, "mfmat5/768/kt1/tile19/coop0/w3/cmp/regs/perm/lw"),
     RT2_VARIANT(334, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 1); x.diag = true; return x; }()>, 768, "mfmat5/768/kt1/tile19/coop0/w3/cmp/regs/perm/diag"),
     RT2_VARIANT(299, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, true); x.fair_prio = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/fair/diag/dpp"),
