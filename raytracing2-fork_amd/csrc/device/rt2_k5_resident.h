@@ -144,6 +144,18 @@ __device__ __forceinline__ bool sweep_kt_res(const RenderParams& p, const h8* re
                                              float& best, int& bi, float& bestK, MfmaDiag& dg, bool upper) {
     static_assert(S.kthr > 0 && S.ymma, "the kthr form");
     const int lane = (int)lane_id();
+    // MfmaSpec::diag: shader clocks of the ray setup (t_wait), the products
+    // with their record reads (t_filt), the exact phase with the Y rebuilds
+    // (t_exact) and the whole sweep (t_swp)
+    [[maybe_unused]] unsigned long long tc = 0, tsw = 0;
+    if constexpr (S.diag) tsw = tc = __builtin_amdgcn_s_memtime();
+    auto stamp = [&](unsigned long long& acc) {
+        if constexpr (S.diag) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            acc += t - tc;
+            tc = t;
+        }
+    };
     const f3 m = cross(d, o);
     MfmaScale sc;
     if (!mfma_scale<S>(p.mfma_A, o, d, m, sc)) return false;
@@ -151,6 +163,7 @@ __device__ __forceinline__ bool sweep_kt_res(const RenderParams& p, const h8* re
     _Float16 tw16;
     kt_frags<S>(d, m, sc, a0, tw16);
     kt_y(d, o, bestK, sc, tw16, y1);
+    stamp(dg.t_wait);
     const int ng = (p.n_tris + 31) >> 5, n_tris = p.n_tris;
     const int nres = S.res_l2 ? min(ng, S.res_groups) : ng;
     cfloat* const tri = (cfloat*)p.tri;
@@ -173,12 +186,14 @@ __device__ __forceinline__ bool sweep_kt_res(const RenderParams& p, const h8* re
             tb += kKtOps * 64;
             const unsigned long long M = kt_group<S>(a0, y1, b0, b1, b2, b3, upper);
             if constexpr (S.diag) dg.groups += 1;
+            stamp(dg.t_filt);
             if constexpr (S.sol == 2) {
                 // speed-of-light probe (WRONG images): no exact phase
                 if (M == 0x123456789ull) best = -best;
                 continue;
             }
             if (M && exact_group<S>(M, G, n_tris, tri, o, d, best, bi, bestK, dg)) kt_y(d, o, bestK, sc, tw16, y1);
+            stamp(dg.t_exact);
         }
     }
     if constexpr (S.res_l2) {
@@ -191,6 +206,7 @@ __device__ __forceinline__ bool sweep_kt_res(const RenderParams& p, const h8* re
             if (M && exact_group<S>(M, G, n_tris, tri, o, d, best, bi, bestK, dg)) kt_y(d, o, bestK, sc, tw16, y1);
         }
     }
+    if constexpr (S.diag) dg.t_swp += __builtin_amdgcn_s_memtime() - tsw;
     return true;
 }
 
@@ -360,6 +376,13 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
             atomicAdd(p.seg_counter + 1, dg.groups);  // (wave, triangle group) sweeps
             atomicAdd(p.seg_counter + 2, dg.hot);     // ... with a passing pair
             atomicAdd(p.seg_counter + 3, dg.exact);   // (wave, triangle) exact tests
+            if constexpr (S.kthr) {
+                atomicAdd(p.seg_counter + 12, dg.t_wait);  // shader clocks: the sweep's ray setup
+                atomicAdd(p.seg_counter + 13, dg.t_filt);  // ... products + record reads
+                atomicAdd(p.seg_counter + 14, dg.t_exact); // ... exact phase + Y rebuilds
+                atomicAdd(p.seg_counter + 15, dg.t_swp);   // ... whole sweeps
+                atomicAdd(p.seg_counter + 16, __builtin_amdgcn_s_memtime() - wl_c0);  // ... the wave's life
+            }
         }
 }
 

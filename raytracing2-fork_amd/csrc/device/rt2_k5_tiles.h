@@ -310,38 +310,35 @@ __device__ __forceinline__ bool sweep_k5_tiles(const RenderParams& p, SH& sh,
 
 // MfmaSpec::tile_flow — the record tiles as a stream with LDS counters instead
 // of a workgroup barrier per tile (round 6; DESIGN.md "LDS record tiles").
-// With one barrier per tile the 12 waves meet 165 times per config C segment,
-// and every meeting drains the SIMDs: the wave that falls behind (age priority,
-// its exact tests) finishes its tile alone while the others wait — 25-33 % of
-// wave cycles in the round-5 phase clocks.  Here a wave waits only for the
-// tile it is about to read, so the waves of a SIMD stay staggered (up to one
-// tile apart with two buffers) and the per-tile drain goes away.
+// With one barrier per tile the 12 waves meet 165 times per config C segment
+// and wait for the slowest of them every time.  Here a wave waits only for
+// the tile it is about to read: the waves drift apart by up to a tile and a
+// wave that is behind is not waited for until it holds the stream up.
 //
 // Every wave walks the same stream of tiles (stream index s: tile s % nt of
 // the segment, buffer s % NB; a segment is nt consecutive indices, so the
-// index runs on across segments) and, per tile: waits until landed[b] says
-// tile s is in buffer b, sweeps it (when it has rays), and releases it
-// (rel[b] += 1).  Tile s may be issued once every wave has released tile
-// s - NB (rel[b] == NW * (s / NB)); the first wave to find it issuable claims
-// it (compare-and-swap on `issued`), issues all its LDS-DMA pieces itself,
-// and publishes landed[b] = s + 1 after its own `s_waitcnt vmcnt(0)` — at the
-// start of its next tile, or at once when it is waiting anyway.  Claims are
-// tried in the middle of a tile (the claimer is then a wave that runs ahead)
-// and in the wait loop (so a tile that nobody has claimed yet cannot stall
-// the stream).  No wave reads a buffer before its tile's claimer has seen the
-// DMA land, and no DMA overwrites a buffer before all NW waves released it.
+// index runs on across segments) and, per tile: waits until all NW shares of
+// tile s have landed in buffer b (landed[b] == NW * (s / NB + 1)), sweeps it
+// (when it has rays), and releases it (rel[b] += 1).  Each wave issues its own
+// share of each tile's LDS-DMA pieces (pc = wave, wave + NW, ...) once every
+// wave has released the buffer's previous tile (rel[b] == NW * (s / NB)), and
+// publishes the share (landed[b] += 1) after its own `s_waitcnt vmcnt(0)`, two
+// groups later or at once when it is waiting anyway.  No wave reads a buffer
+// before every share of its tile has landed, and no DMA overwrites a buffer
+// before all NW waves released it.  MfmaSpec::flow_prio: a wave's issue
+// priority for the next tile follows its finishing rank in this one (the
+// last to finish take the SIMD's issue slots first).
 template <int NB>
 struct TileFlow {
-    uint32_t issued;      // stream indices claimed so far (the next one to issue)
-    uint32_t landed[NB];  // per buffer: 1 + the stream index of the tile whose pieces have all landed there
+    uint32_t landed[NB];  // per buffer: shares landed so far (NW per tile)
     uint32_t rel[NB];     // per buffer: releases so far (NW per tile)
 };
 // the wave's place in the stream (wave-uniform; kept across segments)
 struct FlowWave {
-    uint32_t next = 0;  // stream index of the next tile this wave reads
-    int pend = -1;      // a tile this wave claimed (tile_flow 2: its share) whose landing it has not published yet
-    uint32_t next_issue = 0;  // tile_flow 2: the next tile this wave issues its share of
-    int age = 0;              // tile_flow 2: groups swept since the pending share was issued
+    uint32_t next = 0;        // stream index of the next tile this wave reads
+    uint32_t next_issue = 0;  // ... of the next tile this wave issues its share of
+    int pend = -1;            // a share issued whose landing is not published yet
+    int age = 0;              // groups swept since that share was issued
 };
 
 __device__ __forceinline__ uint32_t lds_acquire(uint32_t* a) {
@@ -354,7 +351,7 @@ __device__ __forceinline__ bool sweep_kt_flow(const RenderParams& p, TL& tl, FL&
                                               bool sweeping, bool upper) {
     static_assert(S.kthr && S.perm_frag && S.tile_groups > 0, "the kthr form with register fragments");
     constexpr int K = S.tile_groups, NW = S.block / 64, NB = S.tile_bufs;
-    const int lane = (int)lane_id();
+    const int lane = (int)lane_id(), wave = (int)(threadIdx.x >> 6);
     // MfmaSpec::diag: shader clocks per phase (MfmaDiag t_wait / t_filt / t_exact / t_swp)
     [[maybe_unused]] unsigned long long tc = 0, tsw = 0;
     if constexpr (S.diag) tsw = tc = __builtin_amdgcn_s_memtime();
@@ -380,20 +377,9 @@ __device__ __forceinline__ bool sweep_kt_flow(const RenderParams& p, TL& tl, FL&
     }
     const int ng = (p.n_tris + 31) >> 5, nt = (ng + K - 1) / K;
     const h8* gsrc = reinterpret_cast<const h8*>(p.mfma_kt_frag) + lane;
-    // every LDS-DMA piece of stream index s (4 per group, 1 KiB each: a lane's
-    // 16 B land at base + 16 lane); the kt records of a tile are contiguous
-    auto issue_tile = [&](uint32_t s) {
-        const int g0 = (int)(s % (uint32_t)nt) * K, gn = min(K, ng - g0), b = (int)(s % NB);
-        const h8* src = gsrc + (size_t)g0 * (kKtOps * 64);
-        for (int pc = 0; pc < kKtOps * gn; pc++)
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + pc * 64),
-                                             (__attribute__((address_space(3))) void*)&tl.rec[b][pc * 64], 16, 0, 0);
-    };
-    // tile_flow 2: every wave issues its own share of each tile's pieces
-    // (round-robin, pc = wave, wave + NW, ...: no wave pays a whole tile's
-    // LDS-DMA issue) and publishes it by landed[b] += 1; a tile is in its
-    // buffer when all NW shares are (landed[b] == NW * (s / NB + 1))
-    const int wave = (int)(threadIdx.x >> 6);
+    // this wave's share of stream index s: pieces pc = wave, wave + NW, ...
+    // (4 per group, 1 KiB each: a lane's 16 B land at base + 16 lane); the kt
+    // records of a tile are contiguous
     auto issue_share = [&](uint32_t s) {
         const int g0 = (int)(s % (uint32_t)nt) * K, gn = min(K, ng - g0), b = (int)(s % NB);
         const h8* src = gsrc + (size_t)g0 * (kKtOps * 64);
@@ -401,19 +387,19 @@ __device__ __forceinline__ bool sweep_kt_flow(const RenderParams& p, TL& tl, FL&
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + pc * 64),
                                              (__attribute__((address_space(3))) void*)&tl.rec[b][pc * 64], 16, 0, 0);
     };
-    auto publish_share = [&]() {
-        [[maybe_unused]] unsigned long long t0 = 0;
-        if constexpr (S.diag) t0 = __builtin_amdgcn_s_memtime();
-        wait_vm0();
-        if constexpr (S.diag) dg.t_pub += __builtin_amdgcn_s_memtime() - t0;
-        if (lane == 0) __hip_atomic_fetch_add(&fl.landed[fw.pend % NB], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        fw.pend = -1;
-    };
     // the wave's part of the stream's upkeep: publish a share that has had
     // time to land (`force`: now), then issue the next share once every wave
     // has released that tile's buffer
     auto upkeep = [&](bool force, bool try_issue) {
-        if (fw.pend >= 0 && (force || fw.age >= 2)) publish_share();
+        if (fw.pend >= 0 && (force || fw.age >= 2)) {
+            [[maybe_unused]] unsigned long long t0 = 0;
+            if constexpr (S.diag) t0 = __builtin_amdgcn_s_memtime();
+            wait_vm0();  // this wave's pieces (its only vector-memory operations in flight) have landed
+            if constexpr (S.diag) dg.t_pub += __builtin_amdgcn_s_memtime() - t0;
+            if (lane == 0)
+                __hip_atomic_fetch_add(&fl.landed[fw.pend % NB], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            fw.pend = -1;
+        }
         if (fw.pend < 0 && try_issue) {
             const uint32_t s = fw.next_issue;
             if (lds_acquire(&fl.rel[s % NB]) == (uint32_t)NW * (s / NB)) {
@@ -430,70 +416,24 @@ __device__ __forceinline__ bool sweep_kt_flow(const RenderParams& p, TL& tl, FL&
             }
         }
     };
-    auto publish = [&]() {
-        if (fw.pend < 0) return;
-        [[maybe_unused]] unsigned long long t0 = 0;
-        if constexpr (S.diag) t0 = __builtin_amdgcn_s_memtime();
-        wait_vm0();  // this wave's pieces (the only vector-memory operations it has in flight) have landed
-        if constexpr (S.diag) dg.t_pub += __builtin_amdgcn_s_memtime() - t0;
-        if (lane == 0)
-            __hip_atomic_store(&fl.landed[fw.pend % NB], (uint32_t)fw.pend + 1u, __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
-        fw.pend = -1;
-    };
-    auto try_claim = [&]() {
-        uint32_t s = lds_acquire(&fl.issued);
-        const uint32_t b = s % NB;
-        if (lds_acquire(&fl.rel[b]) != (uint32_t)NW * (s / NB)) return;  // a wave still reads tile s - NB
-        uint32_t won = 0;
-        if (lane == 0)
-            won = __hip_atomic_compare_exchange_strong(&fl.issued, &s, s + 1u, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
-                                                       __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (!__builtin_amdgcn_readfirstlane(won)) return;
-        s = __builtin_amdgcn_readfirstlane(s);
-        [[maybe_unused]] unsigned long long t0 = 0;
-        if constexpr (S.diag) t0 = __builtin_amdgcn_s_memtime();
-        issue_tile(s);
-        if constexpr (S.diag) {
-            dg.t_issue += __builtin_amdgcn_s_memtime() - t0;
-            dg.claims += 1;
-        }
-        fw.pend = (int)s;
-    };
     for (int t = 0; t < nt; t++) {
         const uint32_t s = fw.next++;
         const int b = (int)(s % NB), gn = min(K, ng - t * K);
         stamp(dg.t_exact);
-        if constexpr (S.tile_flow == 2) {
+        upkeep(true, true);
+        while (lds_acquire(&fl.landed[b]) < (uint32_t)NW * (s / NB + 1u)) {
             upkeep(true, true);
-            while (lds_acquire(&fl.landed[b]) < (uint32_t)NW * (s / NB + 1u)) {
-                upkeep(true, true);
-                __builtin_amdgcn_s_sleep(1);
-            }
-        } else {
-            publish();  // a tile claimed during the previous one: its DMA had half a tile to land
-            while (lds_acquire(&fl.landed[b]) < s + 1u) {
-                if (fw.pend >= 0)
-                    publish();
-                else
-                    try_claim();
-                __builtin_amdgcn_s_sleep(1);
-            }
+            __builtin_amdgcn_s_sleep(1);
         }
         stamp(dg.t_wait);
-        if (S.tile_flow == 1 && S.flow_early && fw.pend < 0) try_claim();  // MfmaSpec::flow_early: a full tile of lead
         if (compute) {
             const h8* tb = &tl.rec[b][lane];
             for (int gi = 0; gi < gn; gi++) {
                 const int G = t * K + gi;
                 const h8 b0 = tb[0], b1 = tb[64], b2 = tb[128], b3 = tb[192];
                 tb += kKtOps * 64;
-                if constexpr (S.tile_flow == 2) {
-                    fw.age++;
-                    upkeep(false, gi == K / 2);
-                } else if (gi == K / 2 && fw.pend < 0) {
-                    try_claim();
-                }
+                fw.age++;
+                upkeep(false, gi == K / 2);
                 const unsigned long long M = kt_group<S>(a0, y1, b0, b1, b2, b3, upper);
                 if constexpr (S.diag) dg.groups += 1;
                 stamp(dg.t_filt);
@@ -520,9 +460,6 @@ __device__ __forceinline__ bool sweep_kt_flow(const RenderParams& p, TL& tl, FL&
         uint32_t r_old = 0;
         if (lane == 0) r_old = __hip_atomic_fetch_add(&fl.rel[b], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         if constexpr (S.flow_prio) {
-            // MfmaSpec::flow_prio: issue priority for the next tile by this
-            // wave's place among the NW that finished this one (the last ones
-            // are behind: they take the SIMD's issue slots first)
             const int rank = (int)(__builtin_amdgcn_readfirstlane(r_old) - (uint32_t)NW * (s / NB));
             const int q = rank * 4 / NW;
             if (q >= 3)
@@ -565,9 +502,7 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
     __shared__ TileFlow<S.tile_bufs> flow;
     FlowWave fw;
     if constexpr (S.tile_flow) {
-        static_assert(S.tile_flow == 1 || S.tile_flow == 2, "tile_flow 1 (claims) or 2 (shares)");
         if (threadIdx.x == 0) {
-            flow.issued = 0;
             for (int b = 0; b < S.tile_bufs; b++) flow.landed[b] = flow.rel[b] = 0;
         }
         __syncthreads();
@@ -648,7 +583,7 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
             shade(L, p, best, bi);
         }
     }
-    // tile_flow: a claim of the next segment's first tile may still be in
+    // tile_flow: a share of the next segment's first tiles may still be in
     // flight; it must land before the workgroup's LDS is given back
     if constexpr (S.tile_flow) wait_vm0();
     const RenderParams& p = kargs<RenderParams>();

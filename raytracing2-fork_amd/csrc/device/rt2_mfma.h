@@ -97,10 +97,8 @@ struct MfmaSpec {
     bool res_l2 = false;    // render_mfma_k5r + kthr: groups beyond res_groups are read from L2 (global loads per
                             // wave) after the resident ones: scenes of up to 256 groups
     bool flow_prio = false;  // tile_flow: issue priority by the wave's finishing rank in the last tile
-    bool flow_early = false; // tile_flow: also claim the next tile right after this one has landed
-    int tile_flow = 0;      // render_mfma_k5t + kthr: the tiles as a stream with LDS counters, no barrier per tile
-                            // (rt2_k5_tiles.h sweep_kt_flow): 1 = one wave claims and issues a whole tile, 2 = every
-                            // wave issues and publishes its share
+    bool tile_flow = false;  // render_mfma_k5t + kthr: the tiles as a stream with LDS counters, no barrier per tile;
+                             // every wave issues and publishes its share of each tile (rt2_k5_tiles.h sweep_kt_flow)
     int sol = 0;            // speed-of-light probes (WRONG images; diag clocks only): 1 = every group reads group
                             // 0's records, 2 = no exact phase, 3 = 2 + only the U term is reduced; marginal-cost
                             // probes (same image): 4 = exact phase twice, 5 = products and reduction twice,
@@ -118,7 +116,7 @@ struct MfmaDiag {
     // reads), the exact phase (with the Y rebuilds), the whole sweep; the
     // wave's whole life in the kernel
     unsigned long long t_wait = 0, t_filt = 0, t_exact = 0, t_swp = 0, t_all = 0;
-    // ... and of that: issuing a claimed tile's pieces, waiting for them to land; claims
+    // ... and of that: issuing the wave's tile shares, waiting for them to land; shares issued
     unsigned long long t_issue = 0, t_pub = 0, claims = 0;
 };
 

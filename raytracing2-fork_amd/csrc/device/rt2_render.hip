@@ -655,6 +655,15 @@ constexpr MfmaSpec kt_tiles_spec(int K, int waves, int sched) {
     x.kthr = sched;
     return x;
 }
+// the round-6 default above 8,192 triangles: the LDS-tiled kernel, kthr 4, each ray's own W, the tiles streamed
+// with LDS counters (MfmaSpec::tile_flow) and issue priority by finishing rank (flow_prio)
+constexpr MfmaSpec kt_tiles_flow() {
+    MfmaSpec x = kt_tiles_spec(19, 3, 4);
+    x.kt_lane_w = true;
+    x.tile_flow = true;
+    x.flow_prio = true;
+    return x;
+}
 // the round-6 defaults: kthr 4, the lean lane state; l2 = the L2 continuation (39..256 groups), fair = rank slabs
 constexpr MfmaSpec kt_res_lean(bool l2, bool fair, bool lane_w = false) {
     MfmaSpec x = kt_res_spec(4, false, l2);
@@ -697,8 +706,10 @@ const Variant kVariants[] = {
     RT2_VARIANT(356, K_MFMA, render_mfma_k5r<kt_res_lean(true, true, true)>, 1024, "mfmarl2/1024/kt4/res38l2/coop4/w4/cmp/fair/dpp/lean/lw"),
     // the default above 8,192 triangles: the LDS-tiled kernel (rt2_k5_tiles.h; 19-group tiles, fragments in
     // registers) with the threshold in the K-slots, each ray's own W in the bound (round 6; round 5: 293)
-    RT2_VARIANT(351, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 4); x.kt_lane_w = true; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw"),
+    RT2_VARIANT(370, K_MFMA, render_mfma_k5t<kt_tiles_flow()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flowp"),
 #ifdef RT2_EXPERIMENTS
+    // round 6's first tiled default (one workgroup barrier per tile; 370 streams the tiles with LDS counters)
+    RT2_VARIANT(351, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 4); x.kt_lane_w = true; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw"),
     // round 6's first kthr defaults (the wave's W in the bound; 353-356 take each ray's own)
     RT2_VARIANT(342, K_MFMA, render_mfma_k5r<kt_res_lean(false, false)>, 1024, "mfmar/1024/kt4/res38/coop4/w4/cmp/dpp/lean"),
     RT2_VARIANT(344, K_MFMA, render_mfma_k5r<kt_res_lean(false, true)>, 1024, "mfmar/1024/kt4/res38/coop4/w4/cmp/fair/dpp/lean"),
@@ -763,21 +774,9 @@ const Variant kVariants[] = {
     RT2_VARIANT(332, K_MFMA, render_mfma_k5t<kt_tiles_spec(19, 3, 4)>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm"),
     RT2_VARIANT(333, K_MFMA, render_mfma_k5t<kt_tiles_spec(16, 4, 1)>, 1024, "mfmat5/1024/kt1/tile16/coop0/w4/cmp/regs/perm"),
     RT2_VARIANT(335, K_MFMA, render_mfma_k5t<kt_tiles_spec(16, 4, 4)>, 1024, "mfmat5/1024/kt4/tile16/coop0/w4/cmp/regs/perm"),
-    // ... the tiles as a stream with LDS counters (MfmaSpec::tile_flow: no barrier per tile), 2 x 19 or 3 x 12 groups
-    RT2_VARIANT(357, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 4); x.kt_lane_w = true; x.tile_flow = 1; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flow"),
-    RT2_VARIANT(358, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(12, 3, 4); x.kt_lane_w = true; x.tile_flow = 1; x.tile_bufs = 3; return x; }()>, 768, "mfmat5/768/kt4/tile12x3/coop0/w3/cmp/regs/perm/lw/flow"),
-    RT2_VARIANT(359, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 4); x.kt_lane_w = true; x.tile_flow = 1; x.diag = true; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flow/diag"),
-    RT2_VARIANT(360, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 4); x.kt_lane_w = true; x.tile_flow = 1; x.flow_early = true; x.diag = true; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flowe/diag"),
-    RT2_VARIANT(361, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(9, 3, 4); x.kt_lane_w = true; x.tile_flow = 1; x.flow_early = true; x.tile_bufs = 4; x.diag = true; return x; }()>, 768, "mfmat5/768/kt4/tile9x4/coop0/w3/cmp/regs/perm/lw/flowe/diag"),
-    RT2_VARIANT(362, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(12, 3, 4); x.kt_lane_w = true; x.tile_flow = 1; x.flow_early = true; x.tile_bufs = 3; x.diag = true; return x; }()>, 768, "mfmat5/768/kt4/tile12x3/coop0/w3/cmp/regs/perm/lw/flowe/diag"),
-    RT2_VARIANT(363, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 4); x.kt_lane_w = true; x.tile_flow = 1; x.flow_prio = true; x.diag = true; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flowp/diag"),
-    RT2_VARIANT(364, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 4); x.kt_lane_w = true; x.tile_flow = 1; x.flow_prio = true; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flowp"),
-    RT2_VARIANT(365, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(9, 3, 4); x.kt_lane_w = true; x.tile_flow = 1; x.flow_prio = true; x.tile_bufs = 4; x.diag = true; return x; }()>, 768, "mfmat5/768/kt4/tile9x4/coop0/w3/cmp/regs/perm/lw/flowp/diag"),
-    RT2_VARIANT(366, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 4); x.kt_lane_w = true; x.tile_flow = 2; x.diag = true; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flow2/diag"),
-    RT2_VARIANT(367, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(12, 3, 4); x.kt_lane_w = true; x.tile_flow = 2; x.tile_bufs = 3; x.diag = true; return x; }()>, 768, "mfmat5/768/kt4/tile12x3/coop0/w3/cmp/regs/perm/lw/flow2/diag"),
-    RT2_VARIANT(368, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 4); x.kt_lane_w = true; x.tile_flow = 2; x.flow_prio = true; x.diag = true; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flow2p/diag"),
-    RT2_VARIANT(369, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 4); x.kt_lane_w = true; x.tile_flow = 2; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flow2"),
-    RT2_VARIANT(370, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 4); x.kt_lane_w = true; x.tile_flow = 2; x.flow_prio = true; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flow2p"),
+    // ... the tiles as a stream with LDS counters (MfmaSpec::tile_flow): with its diagnostic clocks; without flow_prio
+    RT2_VARIANT(368, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_flow(); x.diag = true; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flowp/diag"),
+    RT2_VARIANT(369, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_flow(); x.flow_prio = false; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flow"),
     RT2_VARIANT(352, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 1); x.kt_lane_w = true; return x; }()>, 768, "mfmat5/768/kt1/tile19/coop0/w3/cmp/regs/perm/lw"),
     RT2_VARIANT(334, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 1); x.diag = true; return x; }()>, 768, "mfmat5/768/kt1/tile19/coop0/w3/cmp/regs/perm/diag"),
     RT2_VARIANT(299, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, true); x.fair_prio = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/fair/diag/dpp"),
@@ -845,10 +844,12 @@ constexpr int kMfmaResL2 = 355;    // 39..256 groups (configs W, K): 38 groups r
                                    // (MfmaSpec::res_l2): config W 28.7 vs 46.5 ms, K 306.8 vs 362.1 ms for round 4-5's
                                    // L2-resident 263 (A/B of the wave-W form 337, identical images)
 constexpr int kMfmaResL2Slab = 356;  // ... its rank slabs (fair-share priority)
-constexpr int kMfmaTiles = 351;    // larger scenes: the LDS-tiled kernel (rt2_k5_tiles.h: one 12-wave workgroup per
+constexpr int kMfmaTiles = 370;    // larger scenes: the LDS-tiled kernel (rt2_k5_tiles.h: one 12-wave workgroup per
                                    // CU, 19-group record tiles, fragments in registers) with the threshold in the
-                                   // K-slots and each ray's own W: config C sample 962 vs 1,076 ms, config E sample
-                                   // 1,081 vs 1,230 ms for round 5's 293 (cthr; A/B, identical images)
+                                   // K-slots and each ray's own W (config C sample 962 vs 1,076 ms, config E sample
+                                   // 1,081 vs 1,230 ms for round 5's 293), the tiles streamed with LDS counters and
+                                   // rank priority (full-width config C frame 5,268 vs 5,369 ms, config E 5,447 vs
+                                   // 5,522 ms for 351; A/B, identical images)
 constexpr int kMfma = 227;  // mfma/.../k5/...: the matrix-core filter on v_mfma_f32_32x32x16_f16, 5 products per
                             // 32-ray block (DESIGN.md "The 5-product form"), registers only; larger scenes whose
                             // packed path state cannot hold the launch

@@ -239,9 +239,9 @@ def near_threshold_scene(rt2mod):
     return sd
 
 
-@pytest.mark.parametrize("variant", [227, 351, 353, 354, 355, 356, 293, 342, 344, 345, 346, 228, 231, 233, 212, 213, 217, 260, 261, 262, 263, 243, 250,
+@pytest.mark.parametrize("variant", [227, 370, 353, 354, 355, 356, 351, 293, 342, 344, 345, 346, 228, 231, 233, 212, 213, 217, 260, 261, 262, 263, 243, 250,
                                      252, 280, 282, 298, 320, 321, 322, 323, 325, 326, 329, 330, 332, 336, 337, 340,
-                                     347, 348, 349, 350, 352, 357, 358])
+                                     347, 348, 349, 350, 352, 368, 369])
 def test_near_threshold_scene_bit_exact(rt2mod, oraclemod, torch_cuda, variant):
     if not rt2mod.has_variant(variant):
         pytest.skip(f"variant {variant} not in this build")
