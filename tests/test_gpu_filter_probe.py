@@ -27,6 +27,7 @@ import numpy as np
 import pytest
 
 import filter_probe_lib as fpl
+from conftest import EXPERIMENTS, require_variant
 from test_gpu_parity import assert_exact, oracle_mean
 
 pytestmark = pytest.mark.gpu
@@ -239,12 +240,15 @@ def near_threshold_scene(rt2mod):
     return sd
 
 
-@pytest.mark.parametrize("variant", [227, 370, 353, 354, 355, 356, 351, 293, 342, 344, 345, 346, 228, 231, 233, 212, 213, 217, 260, 261, 262, 263, 243, 250,
-                                     252, 280, 282, 298, 320, 321, 322, 323, 325, 326, 329, 330, 332, 336, 337, 340,
-                                     347, 348, 349, 350, 352, 368, 369])
+# the product's matrix-filter kernels, and in an experiment build its A/B variants too
+NEAR_THRESHOLD_VARIANTS = [227, 370, 353, 354, 355, 356] + (
+    [351, 293, 342, 344, 345, 346, 228, 231, 233, 212, 213, 217, 260, 261, 262, 263, 243, 250, 252, 280, 282, 298, 320,
+     321, 322, 323, 325, 326, 329, 330, 332, 336, 337, 340, 347, 348, 349, 350, 352, 368, 369] if EXPERIMENTS else [])
+
+
+@pytest.mark.parametrize("variant", NEAR_THRESHOLD_VARIANTS)
 def test_near_threshold_scene_bit_exact(rt2mod, oraclemod, torch_cuda, variant):
-    if not rt2mod.has_variant(variant):
-        pytest.skip(f"variant {variant} not in this build")
+    require_variant(rt2mod, variant)
     sd = near_threshold_scene(rt2mod)
     u = rt2mod.offline_uniforms(64, 48, 8, 4, sd.num_triangles)
     u.cameraPos.x, u.cameraPos.y, u.cameraPos.z = 0.0, 0.5, 4.0  # low over the floor: grazing rays
