@@ -351,6 +351,7 @@ __device__ __forceinline__ bool sweep_kt_flow(const RenderParams& p, TL& tl, FL&
                                               bool sweeping, bool upper) {
     static_assert(S.kthr && S.perm_frag && S.tile_groups > 0, "the kthr form with register fragments");
     constexpr int K = S.tile_groups, NW = S.block / 64, NB = S.tile_bufs;
+    static_assert((NB & (NB - 1)) == 0 && NW % 2 == 0, "stream counters: NB a power of two, NW even (wrap-safe)");
     const int lane = (int)lane_id(), wave = (int)(threadIdx.x >> 6);
     // MfmaSpec::diag: shader clocks per phase (MfmaDiag t_wait / t_filt / t_exact / t_swp)
     [[maybe_unused]] unsigned long long tc = 0, tsw = 0;
@@ -421,7 +422,9 @@ __device__ __forceinline__ bool sweep_kt_flow(const RenderParams& p, TL& tl, FL&
         const int b = (int)(s % NB), gn = min(K, ng - t * K);
         stamp(dg.t_exact);
         upkeep(true, true);
-        while (lds_acquire(&fl.landed[b]) < (uint32_t)NW * (s / NB + 1u)) {
+        // (wrap-safe: the counters and stream index are 32-bit and may wrap in
+        // a launch of hours; NB and NW even keep NW * (s / NB) consistent mod 2^32)
+        while ((int32_t)(lds_acquire(&fl.landed[b]) - (uint32_t)NW * (s / NB + 1u)) < 0) {
             upkeep(true, true);
             __builtin_amdgcn_s_sleep(1);
         }
