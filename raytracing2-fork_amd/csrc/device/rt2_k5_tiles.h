@@ -517,11 +517,15 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
     MfmaDiag dg;
     [[maybe_unused]] unsigned long long t_start = 0;
     if constexpr (S.diag) t_start = __builtin_amdgcn_s_memtime();
+    // MfmaSpec::lean (as in render_mfma_k5r): x, y recomputed from the item,
+    // the wave counts its lanes' segments
+    [[maybe_unused]] unsigned long long segs_w = 0;
     for (;;) {
         const RenderParams& p = kargs<RenderParams>();
-        advance(L, p);
+        advance<1, !S.lean>(L, p);
         unsigned long long act = __ballot(L.st == ST_TRACE);
         if (!block_any<NW>(act != 0, vote, vote_parity)) break;
+        if constexpr (S.lean) segs_w += (unsigned long long)__popcll(act);
         const bool coop = act != 0 && __popcll(act) <= (unsigned)S.tail_lanes && __any(L.st == ST_DONE);
         const bool sweeping = act != 0 && !coop;
         bool upper = true;
@@ -531,7 +535,7 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
                     const uint32_t l = lane_id(), nl = (uint32_t)__popcll(act);
                     const bool live = (act >> l) & 1ull;
                     const int to = 4 * (int)(live ? lanes_below(act) : nl + lanes_below(~act));
-                    lane_permute(L, to);
+                    lane_permute<!S.lean, !S.lean>(L, to);
                     act = __ballot(L.st == ST_TRACE);
                 }
                 upper = false;
@@ -573,7 +577,7 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
             coop_each(act, L.o, L.d, p, mybest, mybi);
             if (mine) {
                 L.bounce += 1;
-                L.segs += 1;
+                if constexpr (!S.lean) L.segs += 1;
                 shade(L, p, mybest, mybi);
             }
             continue;
@@ -582,7 +586,7 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
         if (!swept) coop_each(act, ro, rd, p, best, bi);
         if (mine) {
             L.bounce += 1;
-            L.segs += 1;
+            if constexpr (!S.lean) L.segs += 1;
             shade(L, p, best, bi);
         }
     }
@@ -590,7 +594,11 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
     // flight; it must land before the workgroup's LDS is given back
     if constexpr (S.tile_flow) wait_vm0();
     const RenderParams& p = kargs<RenderParams>();
-    flush_counters(L, p);
+    if constexpr (S.lean) {
+        if (lane_id() == 0) atomicAdd(p.seg_counter, segs_w);
+    } else {
+        flush_counters(L, p);
+    }
     if constexpr (S.diag)
         if (lane_id() == 0) {
             atomicAdd(p.seg_counter + 1, dg.groups);  // (wave, triangle group) sweeps

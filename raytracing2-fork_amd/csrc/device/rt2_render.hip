@@ -655,13 +655,21 @@ constexpr MfmaSpec kt_tiles_spec(int K, int waves, int sched) {
     x.kthr = sched;
     return x;
 }
-// the round-6 default above 8,192 triangles: the LDS-tiled kernel, kthr 4, each ray's own W, the tiles streamed
-// with LDS counters (MfmaSpec::tile_flow) and issue priority by finishing rank (flow_prio)
+// the round-6 tiled kernel (above 8,192 triangles): kthr 4, each ray's own W, the tiles streamed with LDS counters
+// (MfmaSpec::tile_flow) and issue priority by finishing rank (flow_prio)
 constexpr MfmaSpec kt_tiles_flow() {
     MfmaSpec x = kt_tiles_spec(19, 3, 4);
     x.kt_lane_w = true;
     x.tile_flow = true;
     x.flow_prio = true;
+    return x;
+}
+// ... at 4 waves per SIMD (1,024 threads) with the lean lane state (128 VGPRs, 1 spilled): the default
+constexpr MfmaSpec kt_tiles_flow4() {
+    MfmaSpec x = kt_tiles_flow();
+    x.block = 1024;
+    x.waves = 4;
+    x.lean = true;
     return x;
 }
 // the round-6 defaults: kthr 4, the lean lane state; l2 = the L2 continuation (39..256 groups), fair = rank slabs
@@ -706,8 +714,10 @@ const Variant kVariants[] = {
     RT2_VARIANT(356, K_MFMA, render_mfma_k5r<kt_res_lean(true, true, true)>, 1024, "mfmarl2/1024/kt4/res38l2/coop4/w4/cmp/fair/dpp/lean/lw"),
     // the default above 8,192 triangles: the LDS-tiled kernel (rt2_k5_tiles.h; 19-group tiles, fragments in
     // registers) with the threshold in the K-slots, each ray's own W in the bound (round 6; round 5: 293)
-    RT2_VARIANT(370, K_MFMA, render_mfma_k5t<kt_tiles_flow()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flowp"),
+    RT2_VARIANT(380, K_MFMA, render_mfma_k5t<kt_tiles_flow4()>, 1024, "mfmat5/1024/kt4/tile19/coop0/w4/cmp/regs/perm/lw/flowp/lean"),
 #ifdef RT2_EXPERIMENTS
+    // the tile stream at 3 waves per SIMD (380 takes 4 with the lean lane state)
+    RT2_VARIANT(370, K_MFMA, render_mfma_k5t<kt_tiles_flow()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flowp"),
     // round 6's first tiled default (one workgroup barrier per tile; 370 streams the tiles with LDS counters)
     RT2_VARIANT(351, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 4); x.kt_lane_w = true; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw"),
     // round 6's first kthr defaults (the wave's W in the bound; 353-356 take each ray's own)
@@ -777,6 +787,9 @@ const Variant kVariants[] = {
     // ... the tiles as a stream with LDS counters (MfmaSpec::tile_flow): with its diagnostic clocks; without flow_prio
     RT2_VARIANT(368, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_flow(); x.diag = true; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flowp/diag"),
     RT2_VARIANT(369, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_flow(); x.flow_prio = false; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flow"),
+    // ... 4 waves per SIMD with 16-group tiles; the lean lane state at 3 waves
+    RT2_VARIANT(381, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_flow4(); x.tile_groups = 16; return x; }()>, 1024, "mfmat5/1024/kt4/tile16/coop0/w4/cmp/regs/perm/lw/flowp/lean"),
+    RT2_VARIANT(382, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_flow(); x.lean = true; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flowp/lean"),
     RT2_VARIANT(352, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 1); x.kt_lane_w = true; return x; }()>, 768, "mfmat5/768/kt1/tile19/coop0/w3/cmp/regs/perm/lw"),
     RT2_VARIANT(334, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 1); x.diag = true; return x; }()>, 768, "mfmat5/768/kt1/tile19/coop0/w3/cmp/regs/perm/diag"),
     RT2_VARIANT(299, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, true); x.fair_prio = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/fair/diag/dpp"),
@@ -844,12 +857,13 @@ constexpr int kMfmaResL2 = 355;    // 39..256 groups (configs W, K): 38 groups r
                                    // (MfmaSpec::res_l2): config W 28.7 vs 46.5 ms, K 306.8 vs 362.1 ms for round 4-5's
                                    // L2-resident 263 (A/B of the wave-W form 337, identical images)
 constexpr int kMfmaResL2Slab = 356;  // ... its rank slabs (fair-share priority)
-constexpr int kMfmaTiles = 370;    // larger scenes: the LDS-tiled kernel (rt2_k5_tiles.h: one 12-wave workgroup per
+constexpr int kMfmaTiles = 380;    // larger scenes: the LDS-tiled kernel (rt2_k5_tiles.h: one 16-wave workgroup per
                                    // CU, 19-group record tiles, fragments in registers) with the threshold in the
                                    // K-slots and each ray's own W (config C sample 962 vs 1,076 ms, config E sample
                                    // 1,081 vs 1,230 ms for round 5's 293), the tiles streamed with LDS counters and
                                    // rank priority (full-width config C frame 5,268 vs 5,369 ms, config E 5,447 vs
-                                   // 5,522 ms for 351; A/B, identical images)
+                                   // 5,522 ms for 351), 4 waves per SIMD with the lean lane state (C frame 5,037 vs
+                                   // 5,237 ms, E 5,285 vs 5,451 ms for 370; A/B, identical images)
 constexpr int kMfma = 227;  // mfma/.../k5/...: the matrix-core filter on v_mfma_f32_32x32x16_f16, 5 products per
                             // 32-ray block (DESIGN.md "The 5-product form"), registers only; larger scenes whose
                             // packed path state cannot hold the launch

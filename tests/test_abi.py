@@ -89,7 +89,7 @@ def test_experiment_variants_not_in_product_build(rt2mod):
     (DESIGN.md §Kernels); A/B variants live in the EXPERIMENTS=1 build."""
     if os.environ.get("RT2_LIB") == "exp":
         return
-    for v in (0, 86, 92, 109, 136, 227, 353, 354, 355, 356, 370):
+    for v in (0, 86, 92, 109, 136, 227, 353, 354, 355, 356, 380):
         assert rt2mod.has_variant(v)
     for v in (213, 217, 231, 243, 252, 260, 261, 262, 263, 282, 298, 130, 131, 132, 133, 134, 135, 137, 138, 139, 143,
               144, 145, 146, 150, 152, 200, 206, 228, 233, 245, 250, 251, 1, 22, 28, 40, 46, 53, 64, 67, 74, 84, 85, 87,

@@ -15,13 +15,13 @@ pytestmark = pytest.mark.gpu
 MFMA = 227
 # every matrix-filter variant of the loaded library runs each case: the
 # product build's automatic kernels (227, the resident 353 / 354 and their L2
-# continuation 355 / 356, the LDS-tiled 370); the experiment build adds its A/B variants
+# continuation 355 / 356, the LDS-tiled 380); the experiment build adds its A/B variants
 # (other drain thresholds, wave counts, record tiles, the kthr forms 320-325)
 
 
 def _mfma_variants():
     """Every matrix-filter variant the loaded library carries (ids 130-399:
-    the product defaults 353-356 / 370 included)."""
+    the product defaults 353-356 / 380 included)."""
     import rt2
     out = []
     for v in range(130, 400):

@@ -129,7 +129,7 @@ def _last_variant(rt2mod, scene):
     return rt2mod.lib().rt2_variant_name(lv.value).decode()
 
 
-AUTO_TILES = "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flowp"  # variant 370: > 8,192 triangles, LDS record tiles
+AUTO_TILES = "mfmat5/1024/kt4/tile19/coop0/w4/cmp/regs/perm/lw/flowp/lean"  # variant 380: > 8,192 triangles, LDS record tiles
 AUTO_RES = "mfmar/1024/kt4/res38/coop4/w4/cmp/dpp/lean/lw"  # 353: <= 38 groups (1,216 triangles), records resident in LDS
 AUTO_RES_SLAB = "mfmar/1024/kt4/res38/coop4/w4/cmp/fair/dpp/lean/lw"  # 354: the same, < 6 items per lane (rank slabs)
 AUTO_RES_L2 = "mfmarl2/1024/kt4/res38l2/coop4/w4/cmp/dpp/lean/lw"  # 355: 39..256 groups, the rest from L2
@@ -404,13 +404,13 @@ def test_frame_split_identical(rt2mod, oraclemod, config_scene, torch_cuda, trav
 
 
 # brute-force kernel variants that change the schedule, not the arithmetic:
-# the product variants (0 = automatic, 86, 92, 227 = the matrix filter, 370 = its LDS-tiled form, 353/354 = its
+# the product variants (0 = automatic, 86, 92, 227 = the matrix filter, 380 = its LDS-tiled form, 353/354 = its
 # LDS-resident forms and 355/356 their L2 continuation, 136 = the scalar path forced) and, in an experiment build, the A/B
 # variants (masked/plk filters, resident LDS, cooperative and team tail modes,
 # split waves, the round-1 slab kernels, occupancy hints)
-BRUTE_VARIANTS = [0, 86, 92, 227, 370, 353, 354, 355, 356, 136] + (
+BRUTE_VARIANTS = [0, 86, 92, 227, 380, 353, 354, 355, 356, 136] + (
     [217, 262, 263, 282, 298, 213, 231, 243, 252, 260, 261, 212, 246, 228, 233, 250, 280, 320, 321, 322, 323, 325, 326,
-     327, 328, 329, 336, 337, 338, 340, 343, 351, 369, 67, 85, 106, 64, 66, 74, 76, 79, 80] if EXPERIMENTS else [])
+     327, 328, 329, 336, 337, 338, 340, 343, 351, 369, 370, 67, 85, 106, 64, 66, 74, 76, 79, 80] if EXPERIMENTS else [])
 
 
 @pytest.mark.parametrize("variant", BRUTE_VARIANTS)
