@@ -424,9 +424,13 @@ __device__ __forceinline__ bool sweep_kt_flow(const RenderParams& p, TL& tl, FL&
         upkeep(true, true);
         // (wrap-safe: the counters and stream index are 32-bit and may wrap in
         // a launch of hours; NB and NW even keep NW * (s / NB) consistent mod 2^32)
+        // (bounded: a wait of 2^24 sleeps, ~1 s, cannot be a slow wave — a
+        // tile takes ~20-40 k clocks — so the kernel traps instead of hanging)
+        uint32_t spins = 0;
         while ((int32_t)(lds_acquire(&fl.landed[b]) - (uint32_t)NW * (s / NB + 1u)) < 0) {
             upkeep(true, true);
             __builtin_amdgcn_s_sleep(1);
+            if (++spins == (1u << 24)) __builtin_trap();
         }
         stamp(dg.t_wait);
         if (compute) {
