@@ -790,6 +790,8 @@ const Variant kVariants[] = {
     // ... 4 waves per SIMD with 16-group tiles; the lean lane state at 3 waves
     RT2_VARIANT(381, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_flow4(); x.tile_groups = 16; return x; }()>, 1024, "mfmat5/1024/kt4/tile16/coop0/w4/cmp/regs/perm/lw/flowp/lean"),
     RT2_VARIANT(382, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_flow(); x.lean = true; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flowp/lean"),
+    RT2_VARIANT(385, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_flow4(); x.flow_prio = false; return x; }()>, 1024, "mfmat5/1024/kt4/tile19/coop0/w4/cmp/regs/perm/lw/flow/lean"),
+    RT2_VARIANT(386, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_flow4(); x.tail_lanes = 4; return x; }()>, 1024, "mfmat5/1024/kt4/tile19/coop4/w4/cmp/regs/perm/lw/flowp/lean"),
     RT2_VARIANT(352, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 1); x.kt_lane_w = true; return x; }()>, 768, "mfmat5/768/kt1/tile19/coop0/w3/cmp/regs/perm/lw"),
     RT2_VARIANT(334, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 1); x.diag = true; return x; }()>, 768, "mfmat5/768/kt1/tile19/coop0/w3/cmp/regs/perm/diag"),
     RT2_VARIANT(299, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, true); x.fair_prio = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/fair/diag/dpp"),
