@@ -90,6 +90,22 @@ __device__ __forceinline__ bool exact_group(unsigned long long M, int G, int n_t
     return __ballot(bestK != bk0) != 0;
 }
 
+// MfmaSpec::phase_prio: the wave's issue priority by its phase (the SIMD's
+// arbiter issues by priority, then age): 1 = the products' phase high, the
+// exact phase and shading low; 2 = the exact phase high; 3 = shading high;
+// 4 = both VALU phases (exact phase, shading) high
+template <MfmaSpec S>
+__device__ __forceinline__ void phase_prio(int phase) {  // 0 products, 1 exact phase, 2 shading
+    if constexpr (S.phase_prio > 0) {
+        const bool hi = (S.phase_prio == 1 && phase == 0) || (S.phase_prio == 2 && phase == 1) ||
+                        (S.phase_prio == 3 && phase == 2) || (S.phase_prio == 4 && phase != 0);
+        if (hi)
+            __builtin_amdgcn_s_setprio(1);
+        else
+            __builtin_amdgcn_s_setprio(0);
+    }
+}
+
 // Closest hit of every lane's ray over all triangles, cthr records from LDS.
 // Returns false (wave-uniform, nothing computed) when a ray is outside the
 // filter's range.
@@ -192,7 +208,11 @@ __device__ __forceinline__ bool sweep_kt_res(const RenderParams& p, const h8* re
                 if (M == 0x123456789ull) best = -best;
                 continue;
             }
-            if (M && exact_group<S>(M, G, n_tris, tri, o, d, best, bi, bestK, dg)) kt_y(d, o, bestK, sc, tw16, y1);
+            if (M) {
+                phase_prio<S>(1);
+                if (exact_group<S>(M, G, n_tris, tri, o, d, best, bi, bestK, dg)) kt_y(d, o, bestK, sc, tw16, y1);
+                phase_prio<S>(0);
+            }
             stamp(dg.t_exact);
         }
     }
@@ -333,12 +353,14 @@ __global__ __launch_bounds__(S.block) __attribute__((amdgpu_waves_per_eu(S.waves
         float best = 1e38f, bestK = 1e38f * 1.0009765625f;
         int bi = -1;
         bool swept;
+        phase_prio<S>(0);
         if constexpr (S.kthr)
             swept = sweep_kt_res<S>(p, rs.rec, ro, rd, best, bi, bestK, dg, upper);
         else
             swept = sweep_k5_res<S>(p, rs.rec, ro, rd, best, bi, bestK, dg, upper);
         // a ray outside the filter's range (wave-uniform): the drain's code
         if (!swept) coop_each(act, ro, rd, p, best, bi);
+        phase_prio<S>(2);
         if (mine) {
             L.bounce += 1;
             if constexpr (!S.lean) L.segs += 1;

@@ -96,6 +96,8 @@ struct MfmaSpec {
                             // fences (the compiler's order)
     bool res_l2 = false;    // render_mfma_k5r + kthr: groups beyond res_groups are read from L2 (global loads per
                             // wave) after the resident ones: scenes of up to 256 groups
+    int phase_prio = 0;      // render_mfma_k5r: issue priority by phase (1 products high, 2 exact phase high,
+                             // 3 shading high; rt2_k5_resident.h phase_prio)
     bool flow_prio = false;  // tile_flow: issue priority by the wave's finishing rank in the last tile
     bool tile_flow = false;  // render_mfma_k5t + kthr: the tiles as a stream with LDS counters, no barrier per tile;
                              // every wave issues and publishes its share of each tile (rt2_k5_tiles.h sweep_kt_flow)

@@ -680,6 +680,13 @@ constexpr MfmaSpec kt_res_lean(bool l2, bool fair, bool lane_w = false) {
     x.kt_lane_w = lane_w;
     return x;
 }
+// the whole-image defaults (353, 355): each ray's own W and issue priority by phase (the exact phase and shading
+// above the products: MfmaSpec::phase_prio 4); the rank-slab forms (354, 356) keep fair-share priority instead
+constexpr MfmaSpec kt_res_prod(bool l2) {
+    MfmaSpec x = kt_res_lean(l2, false, true);
+    x.phase_prio = 4;
+    return x;
+}
 constexpr int kResL2Groups = 256;  // render_mfma_k5r with res_l2: 38 groups resident, the rest from L2
 constexpr Bvh3Spec kBvhDefault{.block = 256, .thresh = 16, .slab = Slab::Markstein, .waves = 5, .diag = false};
 
@@ -708,9 +715,9 @@ const Variant kVariants[] = {
     // records in LDS for the whole launch, 38 groups, the rest read from L2) with the threshold in the K-slots
     // (MfmaSpec::kthr 4: 8 independent products per group, the two 32-ray blocks interleaved; DESIGN.md "The
     // threshold in the K-slots"), the lean lane state; fair-share issue priority for rank slabs
-    RT2_VARIANT(353, K_MFMA, render_mfma_k5r<kt_res_lean(false, false, true)>, 1024, "mfmar/1024/kt4/res38/coop4/w4/cmp/dpp/lean/lw"),
+    RT2_VARIANT(353, K_MFMA, render_mfma_k5r<kt_res_prod(false)>, 1024, "mfmar/1024/kt4/res38/coop4/w4/cmp/dpp/lean/lw/pp4"),
     RT2_VARIANT(354, K_MFMA, render_mfma_k5r<kt_res_lean(false, true, true)>, 1024, "mfmar/1024/kt4/res38/coop4/w4/cmp/fair/dpp/lean/lw"),
-    RT2_VARIANT(355, K_MFMA, render_mfma_k5r<kt_res_lean(true, false, true)>, 1024, "mfmarl2/1024/kt4/res38l2/coop4/w4/cmp/dpp/lean/lw"),
+    RT2_VARIANT(355, K_MFMA, render_mfma_k5r<kt_res_prod(true)>, 1024, "mfmarl2/1024/kt4/res38l2/coop4/w4/cmp/dpp/lean/lw/pp4"),
     RT2_VARIANT(356, K_MFMA, render_mfma_k5r<kt_res_lean(true, true, true)>, 1024, "mfmarl2/1024/kt4/res38l2/coop4/w4/cmp/fair/dpp/lean/lw"),
     // the default above 8,192 triangles: the LDS-tiled kernel (rt2_k5_tiles.h; 19-group tiles, fragments in
     // registers) with the threshold in the K-slots, each ray's own W in the bound (round 6; round 5: 293)
@@ -792,6 +799,11 @@ const Variant kVariants[] = {
     RT2_VARIANT(382, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_flow(); x.lean = true; return x; }()>, 768, "mfmat5/768/kt4/tile19/coop0/w3/cmp/regs/perm/lw/flowp/lean"),
     RT2_VARIANT(385, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_flow4(); x.flow_prio = false; return x; }()>, 1024, "mfmat5/1024/kt4/tile19/coop0/w4/cmp/regs/perm/lw/flow/lean"),
     RT2_VARIANT(386, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_flow4(); x.tail_lanes = 4; return x; }()>, 1024, "mfmat5/1024/kt4/tile19/coop4/w4/cmp/regs/perm/lw/flowp/lean"),
+    // ... issue priority by phase (MfmaSpec::phase_prio 1 / 2 / 3; 353 takes 4); 391 = 353 without it
+    RT2_VARIANT(387, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = kt_res_lean(false, false, true); x.phase_prio = 1; return x; }()>, 1024, "mfmar/1024/kt4/res38/coop4/w4/cmp/dpp/lean/lw/pp1"),
+    RT2_VARIANT(388, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = kt_res_lean(false, false, true); x.phase_prio = 2; return x; }()>, 1024, "mfmar/1024/kt4/res38/coop4/w4/cmp/dpp/lean/lw/pp2"),
+    RT2_VARIANT(389, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = kt_res_lean(false, false, true); x.phase_prio = 3; return x; }()>, 1024, "mfmar/1024/kt4/res38/coop4/w4/cmp/dpp/lean/lw/pp3"),
+    RT2_VARIANT(391, K_MFMA, render_mfma_k5r<kt_res_lean(false, false, true)>, 1024, "mfmar/1024/kt4/res38/coop4/w4/cmp/dpp/lean/lw"),
     RT2_VARIANT(352, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 1); x.kt_lane_w = true; return x; }()>, 768, "mfmat5/768/kt1/tile19/coop0/w3/cmp/regs/perm/lw"),
     RT2_VARIANT(334, K_MFMA, render_mfma_k5t<[] { MfmaSpec x = kt_tiles_spec(19, 3, 1); x.diag = true; return x; }()>, 768, "mfmat5/768/kt1/tile19/coop0/w3/cmp/regs/perm/diag"),
     RT2_VARIANT(299, K_MFMA, render_mfma_k5r<[] { MfmaSpec x = k5_res_spec(4, true); x.fair_prio = true; return x; }()>, 1024, "mfmar/1024/k5/notn/res38/coop4/w4/cmp/cthr/fair/diag/dpp"),

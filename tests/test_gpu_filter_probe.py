@@ -243,7 +243,7 @@ def near_threshold_scene(rt2mod):
 # the product's matrix-filter kernels, and in an experiment build its A/B variants too
 NEAR_THRESHOLD_VARIANTS = [227, 380, 353, 354, 355, 356] + (
     [351, 370, 293, 342, 344, 345, 346, 228, 231, 233, 212, 213, 217, 260, 261, 262, 263, 243, 250, 252, 280, 282, 298, 320,
-     321, 322, 323, 325, 326, 329, 330, 332, 336, 337, 340, 347, 348, 349, 350, 352, 368, 369, 381, 382] if EXPERIMENTS else [])
+     321, 322, 323, 325, 326, 329, 330, 332, 336, 337, 340, 347, 348, 349, 350, 352, 368, 369, 381, 382, 387, 388, 389, 391] if EXPERIMENTS else [])
 
 
 @pytest.mark.parametrize("variant", NEAR_THRESHOLD_VARIANTS)

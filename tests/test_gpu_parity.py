@@ -130,9 +130,9 @@ def _last_variant(rt2mod, scene):
 
 
 AUTO_TILES = "mfmat5/1024/kt4/tile19/coop0/w4/cmp/regs/perm/lw/flowp/lean"  # variant 380: > 8,192 triangles, LDS record tiles
-AUTO_RES = "mfmar/1024/kt4/res38/coop4/w4/cmp/dpp/lean/lw"  # 353: <= 38 groups (1,216 triangles), records resident in LDS
+AUTO_RES = "mfmar/1024/kt4/res38/coop4/w4/cmp/dpp/lean/lw/pp4"  # 353: <= 38 groups (1,216 triangles), records resident in LDS
 AUTO_RES_SLAB = "mfmar/1024/kt4/res38/coop4/w4/cmp/fair/dpp/lean/lw"  # 354: the same, < 6 items per lane (rank slabs)
-AUTO_RES_L2 = "mfmarl2/1024/kt4/res38l2/coop4/w4/cmp/dpp/lean/lw"  # 355: 39..256 groups, the rest from L2
+AUTO_RES_L2 = "mfmarl2/1024/kt4/res38l2/coop4/w4/cmp/dpp/lean/lw/pp4"  # 355: 39..256 groups, the rest from L2
 AUTO_RES_L2_SLAB = "mfmarl2/1024/kt4/res38l2/coop4/w4/cmp/fair/dpp/lean/lw"  # 356: its rank slabs
 
 
